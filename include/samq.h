@@ -1,0 +1,119 @@
+/*
+ * libsamq_hip.so -- C ABI of the MI355X (gfx950) quantized SAM image-encoder hot path.
+ *
+ * Drop-in boundary for the reference's Python/Triton path (zhanglei1172/sam-quantization):
+ * every entry point below names the reference interface it replaces (file:line, relative to
+ * the reference repository).  Conventions:
+ *   - all tensor arguments are DEVICE pointers on the current HIP device, caller-owned and
+ *     caller-allocated (no globals: the reference's shared `workspace`,
+ *     gptq_triton/quant_linear.py:13, is gone, so calls are reentrant);
+ *   - every launch is enqueued on the explicit `stream` (0 = legacy default stream);
+ *     nothing synchronises the host, so a caller may capture any sequence into a hipGraph;
+ *   - return 0 on success, a negative SAMQ_ERR_* on failure; samq_last_error() returns a
+ *     thread-local message.  The Python layer maps SAMQ_ERR_INVALID -> AssertionError
+ *     (the reference's shape asserts, quant_linear.py:378-399), SAMQ_ERR_UNSUPPORTED ->
+ *     NotImplementedError (quant_linear.py:72-73, fused_attention.py:134-135) and
+ *     SAMQ_ERR_HIP -> RuntimeError.
+ * Data types: "f16" = IEEE binary16, "f32" = binary32; int4 weights use the reference's
+ * GPTQ packing (qweight int32 (K/8,N), qzeros int32 (G,N/8), scales f16 (G,N),
+ * gptq4sam.py:434-497) -- repacked once per layer by samq_w4_repack.
+ */
+#ifndef SAMQ_H
+#define SAMQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAMQ_OK 0
+#define SAMQ_ERR_INVALID (-1)
+#define SAMQ_ERR_UNSUPPORTED (-2)
+#define SAMQ_ERR_HIP (-3)
+
+/* GEMM epilogues (y = acc * scale[n] + bias[n]) */
+#define SAMQ_EPI_BIAS 0        /* C f16  = y                        (QuantLinear.forward)     */
+#define SAMQ_EPI_BIAS_GELU 1   /* C f16  = GELU_erf(y)              (MLPBlock lin1 + act)     */
+#define SAMQ_EPI_RESADD_F32 2  /* C f32 += y (in place)             (Block residual adds)     */
+#define SAMQ_EPI_F32 3         /* C f32  = y                                                  */
+
+/* Thread-local description of the last failure on this thread ("" if none). */
+const char* samq_last_error(void);
+/* ABI version of this library (major*100 + minor). */
+int samq_version(void);
+
+/* ---------------------------------------------------------------- W4A16 (GPTQ int4) */
+
+/* Number of int32 words of the repacked weight of a K x N layer (= K*N/8). */
+size_t samq_w4_packed_words(int K, int N);
+
+/* Repack a reference `QuantLinear.qweight` (int32 (K/8, N), gptq_triton/quant_linear.py:81-85)
+ * into the kernel's MFMA-fragment order.  K % 64 == 0, N % 32 == 0.  Called once per layer
+ * by load_quant (replaces the reference's per-call B-tile addressing, quant_linear.py:292-294). */
+int samq_w4_repack(const int32_t* qweight, int32_t* packed, int K, int N, hipStream_t stream);
+
+/* C = epilogue(A[M,K] (f16, row stride lda) x W4[K,N]).  Replaces triton_matmul4 +
+ * matmul4_kernel (gptq_triton/quant_linear.py:355-437, 231-352) and the separate `c + bias`
+ * (:434-435).  wpacked from samq_w4_repack; scales f16 (G,N); qzeros int32 (G,N/8);
+ * bias f16 (N) or NULL; groupsize -1 (== K) or a multiple of 64.  C is f16 for
+ * SAMQ_EPI_BIAS / SAMQ_EPI_BIAS_GELU and f32 (row stride ldc) for the F32 epilogues.
+ * Shapes: K % 64 == 0, N % 32 == 0 (a superset of the reference's K%128/N%256). */
+int samq_w4a16_gemm(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                    const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N,
+                    int K, int groupsize, int epilogue, hipStream_t stream);
+
+/* Same with an explicit tile configuration (0 = automatic); for tuning and tests.
+ * 1: 256x256 (8 waves)  2: 256x128  3: 128x128  4: 64x64  5: 64x32  6: 128x256. */
+int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                        const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M,
+                        int N, int K, int groupsize, int epilogue, int cfg, hipStream_t stream);
+
+/* ---------------------------------------------------------------- normalisation */
+
+/* y[r,:] = LayerNorm(x[r,:]) * gamma + beta over C channels (row stride C), f32 statistics.
+ * flags: SAMQ_LN_IN_F16 -> x is f16 (else f32); SAMQ_LN_OUT_F32 -> y is f32 (else f16).
+ * gamma/beta f32.  Replaces nn.LayerNorm(eps=1e-6) of Block.norm1/norm2
+ * (segment_anything/modeling/image_encoder.py:184,187,194,205; build_sam.py:72) and the
+ * channel LayerNorm2d of the neck on NHWC tokens (segment_anything/modeling/common.py:31-43). */
+#define SAMQ_LN_IN_F16 1
+#define SAMQ_LN_OUT_F32 2
+int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                   int C, float eps, int flags, hipStream_t stream);
+
+/* ---------------------------------------------------------------- attention */
+
+/* Multi-head attention with in-kernel decomposed relative-position bias over an image token
+ * grid, windowed or global, reading Q/K/V straight from the qkv projection output.
+ * Replaces QuantAttention.forward's attention part -- add_decomposed_rel_pos + the Triton
+ * `_fwd_kernel1` + `forward` (gptq_triton/fused_attention.py:46-80, 107-149, 159-358) -- AND
+ * the window_partition / window_unpartition copies around it
+ * (segment_anything/modeling/image_encoder.py:195-202, 282-333):
+ *   qkv  f16 [B, H, W, 3, heads, hd]  (the qkv Linear output, natural token order)
+ *   out  f16 [B, H, W, heads*hd]      (natural token order; window padding cropped)
+ *   window = 0: global attention over the H x W grid (requires H == W, H % 16 == 0);
+ *   window = S > 0: attention inside S x S windows of the grid zero-padded to a multiple of S;
+ *     padded tokens are keys/values whose q/k/v equal the qkv bias (the reference projects the
+ *     zero-padded LayerNorm output), given by qkv_bias (f16 [3*heads*hd]) or zeros if NULL;
+ *   rel_pos_h / rel_pos_w f16 [2*side-1, hd] with side = window or H; the width term uses the
+ *     query ROW as the table index (reference quirk, image_encoder.py:402 /
+ *     fused_attention.py:78).  hd in {64, 80}; side <= 64 and (window == 0 => side % 16 == 0).
+ *   sm_scale multiplies q.k (the reference passes head_dim**-0.5). */
+int samq_rel_attention(const void* qkv, const void* qkv_bias, const void* rel_pos_h,
+                       const void* rel_pos_w, void* out, int B, int H, int W, int heads, int hd,
+                       int window, float sm_scale, hipStream_t stream);
+
+/* Reference functional API `fused_attention.forward(inp, pos_emb1, pos_emb2, head_num,
+ * hidden_dim, sm_scale)` (gptq_triton/fused_attention.py:312-358): attention over each of B
+ * independent S x S grids with PRECOMPUTED bias terms rel_h, rel_w f16 [B*heads, S, S, S]
+ * (bias[m, n] = rel_h[m, n // S] + rel_w[m, n % S]).  inp f16 [B, S, S, 3*heads*hd],
+ * out f16 [B, S, S, heads*hd]. */
+int samq_attention_relbias(const void* inp, const void* rel_h, const void* rel_w, void* out, int B,
+                           int S, int heads, int hd, float sm_scale, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAMQ_H */

@@ -1,0 +1,62 @@
+// Shared device helpers and the C-ABI error plumbing for libsamq_hip.so (gfx950 / CDNA4).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/samq.h"
+
+namespace samq {
+
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float float16_t __attribute__((ext_vector_type(16)));
+typedef int int4_t __attribute__((ext_vector_type(4)));
+typedef int int16_t_v __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#define SAMQ_GLOBAL __attribute__((address_space(1)))
+#define SAMQ_LDS __attribute__((address_space(3)))
+
+// ---------------------------------------------------------------- error state
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_hip(hipError_t e, const char* what);
+
+#define SAMQ_REQUIRE(cond, code, msg)                  \
+  do {                                                 \
+    if (!(cond)) return ::samq::fail((code), (msg));   \
+  } while (0)
+
+#define SAMQ_LAUNCH_CHECK(what) \
+  do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return ::samq::check_hip(_e, what); } while (0)
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ float gelu_erf(float x) {
+  // nn.GELU() default (exact erf form), reference segment_anything/modeling/common.py:25-26
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D workgroup id: consecutive logical ids share an XCD
+// (MI355X deals workgroups round-robin over 8 XCDs; speed only, never correctness).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, k = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+}  // namespace samq

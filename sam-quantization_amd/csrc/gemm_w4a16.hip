@@ -1,0 +1,343 @@
+// W4A16 GEMM for GPTQ-packed int4 weights on gfx950 fp16 MFMA.
+//
+// Replaces the reference's Triton `matmul4_kernel` + `triton_matmul4`
+// (gptq_triton/quant_linear.py:231-352, 355-437):  C[M,N] = A[M,K] . W[K,N] (+bias, ...)
+// with W[k,n] = s[g,n] * (q[k,n] - zp[g,n]),  q = (qweight[k/8,n] >> 4(k%8)) & 15,
+// zp = ((qzeros[g,n/8] >> 4(n%8)) & 15) + 1.
+//
+// Numerics (deliberately NOT the reference's fp16 dequant `fp16(q*s) - fp16(zp*s)`, which
+// is the dominant error of the reference path): the MFMA multiplies
+// fp16 activations by the EXACT small integers (q - zp) in [-16, 15], accumulates in fp32,
+// and applies the per-channel scale in the fp32 epilogue (groupsize == K).  With groups
+// (groupsize < K) the integer is scaled once, in fp16, per group: fp16((q - zp) * s).
+//
+// Design (MI355X-first, not a translation of the Triton tiling):
+//  * weights are repacked once at load (samq_w4_repack) into MFMA-fragment order: one
+//    dwordx4 per lane holds the 4 k16-steps of its B column for a 64-deep K tile, with the
+//    nibbles interleaved so that ((w >> 4i) & 0x000F000F) | 0x64006400 is directly the fp16
+//    pair (1024+q[2i], 1024+q[2i+1]) -> 7 VALU ops unpack 8 weights, 4 v_pk_add_f16 remove
+//    the zero point.  B never touches LDS: each wave streams its own fragments from L2.
+//  * A is staged global->LDS with global_load_lds_dwordx4 (no VGPR round trip), double
+//    buffered, XOR-swizzled on the SOURCE address (LDS image lane-linear) so the
+//    ds_read_b128 fragment reads of v_mfma_f32_32x32x16_f16 are bank-conflict free.
+//  * wave tiles are >=128 rows (except small fallback configs) so the in-register unpack of
+//    each B word is amortised over >=4 MFMAs (VALU:MFMA issue ~1:3).
+//  * fused epilogues: +bias, +bias+GELU(erf), and fp32 residual accumulate (x += y) so the
+//    residual stream never takes an extra HBM round trip.
+//  * XCD-aware bijective blockIdx remap: consecutive tiles (same A rows) share an L2.
+#include "common.h"
+
+namespace samq {
+
+// ------------------------------------------------------------------ repack
+// packed word index ((nt * (K/64) + kb) * 64 + lane) * 4 + s   holds column n = nt*32 + (lane&31),
+// k = kb*64 + 16*s + 8*(lane>>5) + {0..7}, nibble order [k0,k2,k4,k6 | k1,k3,k5,k7].
+__global__ void w4_repack_kernel(const uint32_t* __restrict__ qweight, uint32_t* __restrict__ out,
+                                 int K, int N) {
+  const int64_t total = (int64_t)K * N / 8;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int s = idx & 3;
+    const int lane = (idx >> 2) & 63;
+    const int64_t blk = idx >> 8;             // nt * (K/64) + kb
+    const int kbs = K / 64;
+    const int kb = (int)(blk % kbs);
+    const int nt = (int)(blk / kbs);
+    const int n = nt * 32 + (lane & 31);
+    const int k0 = kb * 64 + 16 * s + 8 * (lane >> 5);
+    const uint32_t w = qweight[(int64_t)(k0 >> 3) * N + n];
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o |= ((w >> (8 * i)) & 0xFu) << (4 * i);             // q[2i]   -> bits 4i
+      o |= ((w >> (8 * i + 4)) & 0xFu) << (16 + 4 * i);    // q[2i+1] -> bits 16+4i
+    }
+    out[idx] = o;
+  }
+}
+
+// ------------------------------------------------------------------ GEMM
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
+void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
+                       const u32x4* __restrict__ Wp,
+                       const _Float16* __restrict__ scales,
+                       const uint32_t* __restrict__ qzeros,
+                       const _Float16* __restrict__ bias,
+                       void* __restrict__ Cout, int64_t ldc,
+                       int M, int N, int K, int groupsize) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M;
+  constexpr int WN = BN / WAVES_N;
+  constexpr int TM = WM / 32;
+  constexpr int TN = WN / 32;
+  constexpr int BK = 64;
+  constexpr int ROWB = BK * 2;                 // 128 bytes per A row in LDS
+  constexpr int TILE_BYTES = BM * ROWB;
+  constexpr int GLDS_PER_WAVE = BM / 8 / NW;   // 1 KiB (8 rows) per wave-instruction
+  static_assert(TM >= 1 && TN >= 1 && GLDS_PER_WAVE >= 1, "bad tile");
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int nwg = tiles_m * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, nwg);
+  const int tm = bid / tiles_n;
+  const int tn = bid % tiles_n;
+  const int m0 = tm * BM;
+  const int n0 = tn * BN;
+  const int kt_count = K / BK;
+
+  // ---- A staging: this wave's global_load_lds sources (row clamp at M-1)
+  const _Float16* a_src[GLDS_PER_WAVE];
+  int a_dst[GLDS_PER_WAVE];
+#pragma unroll
+  for (int i = 0; i < GLDS_PER_WAVE; ++i) {
+    const int r0 = (wave * GLDS_PER_WAVE + i) * 8;
+    const int row = r0 + (lane >> 3);
+    const int p = lane & 7;
+    const int c = p ^ ((row >> 1) & 7);
+    int gr = m0 + row;
+    gr = gr < M ? gr : M - 1;
+    a_src[i] = A + (int64_t)gr * lda + c * 8;
+    a_dst[i] = r0 * ROWB;
+  }
+  auto stage_a = [&](int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < GLDS_PER_WAVE; ++i) {
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(a_src[i] + kt * BK),
+                                       (SAMQ_LDS void*)(smem + buf * TILE_BYTES + a_dst[i]), 16, 0, 0);
+    }
+  };
+
+  // ---- B fragments (packed): per n-tile one dwordx4 per lane per K tile
+  const int ncol_tile0 = (n0 + wn * WN) / 32;
+  const u32x4* b_ptr[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) b_ptr[t] = Wp + ((int64_t)(ncol_tile0 + t) * kt_count) * 64 + lane;
+
+  // per-lane output column of each n-tile
+  int col[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+
+  auto load_zc = [&](int g, half2_t* zc, half2_t* sc) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const uint32_t zw = qzeros[(int64_t)g * (N / 8) + (col[t] >> 3)];
+      const int zp = (int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1;
+      const _Float16 z = (_Float16)(1024 + zp);
+      zc[t] = half2_t{z, z};
+      if (GROUPED) {
+        const _Float16 s = scales[(int64_t)g * N + col[t]];
+        sc[t] = half2_t{s, s};
+      }
+    }
+  };
+
+  half2_t zc[TN], sc[TN];
+  load_zc(0, zc, sc);
+  int cur_group = 0;
+
+  float16_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // LDS read offsets for the A fragments of this wave (row part), k-chunk added per step
+  int a_row[TM];
+  int a_swz[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_row[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
+  }
+  const int hsel = lane >> 5;
+
+  // prologue
+  stage_a(0, 0);
+  u32x4 bcur[TN], bnext[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) bcur[t] = b_ptr[t][0];
+  __syncthreads();
+
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < kt_count) {
+      stage_a(kt + 1, buf ^ 1);
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bnext[t] = b_ptr[t][(int64_t)(kt + 1) * 64];
+    }
+    if (GROUPED) {
+      const int g = (kt * BK) / groupsize;
+      if (g != cur_group) {
+        load_zc(g, zc, sc);
+        cur_group = g;
+      }
+    }
+    const char* abase = smem + buf * TILE_BYTES;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      half8_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int c = 2 * s + hsel;
+        af[i] = *(const half8_t*)(abase + a_row[i] + ((c ^ a_swz[i]) << 4));
+      }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const uint32_t w = bcur[t][s];
+        half8_t bf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t bits = ((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u;
+          half2_t h = __builtin_bit_cast(half2_t, bits) - zc[t];
+          if (GROUPED) h = h * sc[t];
+          bf[2 * i] = h[0];
+          bf[2 * i + 1] = h[1];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf, acc[i][t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < kt_count) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bcur[t] = bnext[t];
+    }
+  }
+
+  // ---- epilogue
+  float csc[TN], cb[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    csc[t] = GROUPED ? 1.0f : (float)scales[col[t]];
+    cb[t] = bias ? (float)bias[col[t]] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+      if (row >= M) continue;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        float v = acc[i][t][r] * csc[t] + cb[t];
+        if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_erf(v);
+        if (EPI == SAMQ_EPI_RESADD_F32) {
+          float* cp = (float*)Cout + (int64_t)row * ldc + col[t];
+          *cp = *cp + v;
+        } else if (EPI == SAMQ_EPI_F32) {
+          ((float*)Cout)[(int64_t)row * ldc + col[t]] = v;
+        } else {
+          ((_Float16*)Cout)[(int64_t)row * ldc + col[t]] = (_Float16)v;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ dispatch
+struct GemmArgs {
+  const _Float16* A; int64_t lda; const u32x4* Wp; const _Float16* scales; const uint32_t* qzeros;
+  const _Float16* bias; void* C; int64_t ldc; int M, N, K, groupsize;
+};
+
+template <int BM, int BN, int WMW, int WNW, int EPI, bool GR>
+static int launch_cfg(const GemmArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  hipLaunchKernelGGL((w4a16_gemm_kernel<BM, BN, WMW, WNW, EPI, GR>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize);
+  SAMQ_LAUNCH_CHECK("w4a16_gemm launch");
+  return SAMQ_OK;
+}
+
+template <int EPI, bool GR>
+static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 1: return launch_cfg<256, 256, 2, 4, EPI, GR>(a, st);
+    case 2: return launch_cfg<256, 128, 2, 2, EPI, GR>(a, st);
+    case 3: return launch_cfg<128, 128, 2, 2, EPI, GR>(a, st);
+    case 4: return launch_cfg<64, 64, 2, 2, EPI, GR>(a, st);
+    case 5: return launch_cfg<64, 32, 2, 1, EPI, GR>(a, st);
+    case 6: return launch_cfg<128, 256, 1, 4, EPI, GR>(a, st);
+    default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown tile config");
+  }
+}
+
+static int pick_cfg(int M, int N) {
+  if (N % 256 == 0 && M >= 4096) return 1;
+  if (N % 128 == 0 && M >= 2048) return 2;
+  if (N % 128 == 0) return 3;
+  if (N % 64 == 0) return 4;
+  return 5;
+}
+
+static int cfg_bn(int cfg) {
+  switch (cfg) { case 1: return 256; case 2: return 128; case 3: return 128; case 4: return 64;
+                 case 5: return 32; case 6: return 256; default: return 0; }
+}
+
+}  // namespace samq
+
+using namespace samq;
+
+extern "C" size_t samq_w4_packed_words(int K, int N) { return (size_t)K * (size_t)N / 8; }
+
+extern "C" int samq_w4_repack(const int32_t* qweight, int32_t* packed, int K, int N, hipStream_t stream) {
+  SAMQ_REQUIRE(qweight && packed, SAMQ_ERR_INVALID, "w4_repack: null pointer");
+  SAMQ_REQUIRE(K > 0 && N > 0 && K % 64 == 0, SAMQ_ERR_INVALID, "w4_repack: K must be a positive multiple of 64");
+  SAMQ_REQUIRE(N % 32 == 0, SAMQ_ERR_INVALID, "w4_repack: N must be a multiple of 32");
+  const int64_t total = (int64_t)K * N / 8;
+  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(w4_repack_kernel, dim3(blocks), dim3(256), 0, stream, (const uint32_t*)qweight,
+                     (uint32_t*)packed, K, N);
+  SAMQ_LAUNCH_CHECK("w4_repack launch");
+  return SAMQ_OK;
+}
+
+extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                                   const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N,
+                                   int K, int groupsize, int epilogue, int cfg, hipStream_t stream) {
+  SAMQ_REQUIRE(A && wpacked && scales && qzeros && C, SAMQ_ERR_INVALID, "w4a16_gemm: null pointer");
+  SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0, SAMQ_ERR_INVALID, "w4a16_gemm: bad shape");
+  SAMQ_REQUIRE(K % 64 == 0, SAMQ_ERR_INVALID, "w4a16_gemm: K must be a multiple of 64");
+  SAMQ_REQUIRE(N % 32 == 0, SAMQ_ERR_INVALID, "w4a16_gemm: N must be a multiple of 32");
+  SAMQ_REQUIRE(lda >= K && lda % 8 == 0 && ((uintptr_t)A & 15) == 0, SAMQ_ERR_INVALID,
+               "w4a16_gemm: A must be 16-byte aligned with lda >= K, lda % 8 == 0");
+  SAMQ_REQUIRE(ldc >= N, SAMQ_ERR_INVALID, "w4a16_gemm: ldc < N");
+  if (groupsize == -1) groupsize = K;
+  SAMQ_REQUIRE(groupsize > 0 && (groupsize == K || groupsize % 64 == 0), SAMQ_ERR_INVALID,
+               "w4a16_gemm: groupsize must be -1, K, or a multiple of 64");
+  if (M == 0) return SAMQ_OK;
+  if (cfg <= 0) cfg = pick_cfg(M, N);
+  SAMQ_REQUIRE(cfg_bn(cfg) > 0 && N % cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a16_gemm: N not divisible by tile");
+  GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
+             (const _Float16*)bias, C, ldc, M, N, K, groupsize};
+  const bool gr = groupsize != K;
+  switch (epilogue) {
+    case SAMQ_EPI_BIAS: return gr ? launch_epi<SAMQ_EPI_BIAS, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_BIAS, false>(a, cfg, stream);
+    case SAMQ_EPI_BIAS_GELU: return gr ? launch_epi<SAMQ_EPI_BIAS_GELU, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_BIAS_GELU, false>(a, cfg, stream);
+    case SAMQ_EPI_RESADD_F32: return gr ? launch_epi<SAMQ_EPI_RESADD_F32, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_RESADD_F32, false>(a, cfg, stream);
+    case SAMQ_EPI_F32: return gr ? launch_epi<SAMQ_EPI_F32, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_F32, false>(a, cfg, stream);
+    default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown epilogue");
+  }
+}
+
+extern "C" int samq_w4a16_gemm(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                               const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N, int K,
+                               int groupsize, int epilogue, hipStream_t stream) {
+  return samq_w4a16_gemm_cfg(A, lda, wpacked, scales, qzeros, bias, C, ldc, M, N, K, groupsize, epilogue, 0, stream);
+}

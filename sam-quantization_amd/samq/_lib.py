@@ -1,0 +1,88 @@
+"""ctypes binding of libsamq_hip.so (the C ABI declared in include/samq.h).
+
+The library is built in-tree (``make -C sam-quantization_amd`` or ``__graft_entry__.build()``)
+and loaded from this directory.  There is NO fallback: if the library is missing or fails to
+load, importing the product ops raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libsamq_hip.so"
+
+SAMQ_OK = 0
+SAMQ_ERR_INVALID = -1
+SAMQ_ERR_UNSUPPORTED = -2
+SAMQ_ERR_HIP = -3
+
+EPI_BIAS = 0
+EPI_BIAS_GELU = 1
+EPI_RESADD_F32 = 2
+EPI_F32 = 3
+
+LN_IN_F16 = 1
+LN_OUT_F32 = 2
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+
+# name -> (restype, argtypes); must match include/samq.h exactly
+SIGNATURES = {
+    "samq_last_error": (ctypes.c_char_p, []),
+    "samq_version": (_i32, []),
+    "samq_w4_packed_words": (ctypes.c_size_t, [_i32, _i32]),
+    "samq_w4_repack": (_i32, [_vp, _vp, _i32, _i32, _vp]),
+    "samq_w4a16_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "samq_w4a16_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
+    "samq_rel_attention": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp]),
+    "samq_attention_relbias": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _f32, _vp]),
+}
+
+
+class SamqError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise loudly if it is unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"samq: HIP library not found at {LIB_PATH}; build it with "
+            f"`make -C {LIB_PATH.parent.parent}` (hipcc --offload-arch=gfx950). "
+            "There is no CPU or PyTorch fallback.")
+    lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | getattr(os, "RTLD_GLOBAL", 0))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> None:
+    """Map a C status to the reference's exception types (see include/samq.h)."""
+    if status == SAMQ_OK:
+        return
+    msg = load().samq_last_error().decode(errors="replace")
+    if what:
+        msg = f"{what}: {msg}"
+    if status == SAMQ_ERR_INVALID:
+        raise AssertionError(msg)
+    if status == SAMQ_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise SamqError(msg)
+
+
+def exported_symbols():
+    return list(SIGNATURES)

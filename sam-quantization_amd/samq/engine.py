@@ -1,0 +1,187 @@
+"""Fused HIP forward of a quantized SAM ViT image encoder (the hot path).
+
+Replaces, for a whole ``ImageEncoderViT`` (reference ``image_encoder.py:106-118``) after
+``load_quant``, the reference's per-module dataflow (~20 launches and several
+partition/permute/pad copies per block, fp16 residual) by 7 launches per block:
+
+    xn  = LN1(x)                      samq_layernorm      f32 -> f16
+    qkv = xn . Wqkv + b               samq_w4a16_gemm     EPI_BIAS         (natural token order)
+    a   = attn(qkv)                   samq_rel_attention  windowed/global, rel-pos in-kernel,
+                                                          window pad/crop folded into addressing
+    x  += a . Wproj + b               samq_w4a16_gemm     EPI_RESADD_F32   (fp32 residual in place)
+    xn  = LN2(x)                      samq_layernorm
+    h   = GELU(xn . W1 + b1)          samq_w4a16_gemm     EPI_BIAS_GELU
+    x  += h . W2 + b2                 samq_w4a16_gemm     EPI_RESADD_F32
+
+The residual stream ``x`` stays fp32 in HBM (precision: SURVEY.md §7 "Hard parts").
+Patch embedding and the neck (0.3 % of the FLOPs) run as im2col + hipBLASLt GEMMs via torch
+on the GPU plus the HIP LayerNorm; they are the next rows to move into HIP.
+All activation buffers are allocated once per batch size and reused; ``capture()`` records the
+whole forward into a HIP graph for launch-overhead-free replay.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from .quant_linear import QuantLinear
+
+
+class _BlockPlan:
+    __slots__ = ("ln1_w", "ln1_b", "ln1_eps", "qkv", "proj", "relh", "relw", "heads", "window", "scale",
+                 "ln2_w", "ln2_b", "ln2_eps", "lin1", "lin2", "qkv_bias")
+
+
+class EncoderEngine:
+    def __init__(self, enc):
+        from .fused_attention import QuantAttention
+        self.enc = enc
+        self.device = enc.pos_embed.device if enc.pos_embed is not None else next(enc.parameters()).device
+        self.C = enc.embed_dim
+        self.grid = enc.img_size // enc.patch_size
+        self.plans = []
+        for blk in enc.blocks:
+            attn = blk.attn
+            p = _BlockPlan()
+            if isinstance(attn, QuantAttention):
+                qkv, proj = attn.qkv_proj, attn.o_proj
+            else:
+                qkv, proj = attn.qkv, attn.proj
+            for lin in (qkv, proj, blk.mlp.lin1, blk.mlp.lin2):
+                if not isinstance(lin, QuantLinear):
+                    raise TypeError("EncoderEngine needs every encoder Linear quantized (load_quant / make_quant)")
+                lin.prepare()
+            if not attn.use_rel_pos:
+                raise NotImplementedError
+            p.qkv, p.proj, p.lin1, p.lin2 = qkv, proj, blk.mlp.lin1, blk.mlp.lin2
+            p.qkv_bias = qkv.bias
+            p.heads = attn.num_heads
+            p.scale = float(attn.scale)
+            p.window = blk.window_size
+            side = blk.window_size if blk.window_size > 0 else self.grid
+            p.relh, p.relw = self._tables(attn, side)
+            p.ln1_w, p.ln1_b, p.ln1_eps = self._ln(blk.norm1)
+            p.ln2_w, p.ln2_b, p.ln2_eps = self._ln(blk.norm2)
+            self.plans.append(p)
+        pe = enc.patch_embed.proj
+        self.patch = pe.kernel_size[0]
+        self.pe_w = pe.weight.detach().reshape(pe.weight.shape[0], -1).to(torch.float16).contiguous()
+        self.pe_b = pe.bias.detach().float() if pe.bias is not None else None
+        self.pos = enc.pos_embed.detach().float() if enc.pos_embed is not None else None
+        n0, n1, n2, n3 = enc.neck
+        self.n0_w = n0.weight.detach().reshape(n0.weight.shape[0], -1).to(torch.float16).contiguous()
+        self.n1 = (n1.weight.detach().float().contiguous(), n1.bias.detach().float().contiguous(), float(n1.eps))
+        self.n2_w = n2.weight.detach().reshape(n2.weight.shape[0], -1).to(torch.float16).contiguous()
+        self.n3 = (n3.weight.detach().float().contiguous(), n3.bias.detach().float().contiguous(), float(n3.eps))
+        self.out_chans = n0.weight.shape[0]
+        self._bufs = {}
+        self._key = self._make_key(enc)
+
+    # ---------------------------------------------------------------- helpers
+    @staticmethod
+    def _make_key(enc):
+        return tuple((id(m), getattr(m, "qweight", None) is not None and m.qweight._version)
+                     for m in enc.modules() if isinstance(m, QuantLinear))
+
+    def valid_for(self, enc) -> bool:
+        return enc is self.enc and self._make_key(enc) == self._key
+
+    @staticmethod
+    def _ln(norm):
+        return (norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous(), float(norm.eps))
+
+    @staticmethod
+    def _tables(attn, side):
+        def fit(tab):
+            span = 2 * side - 1
+            t = tab.detach().float()
+            if t.shape[0] != span:
+                t = F.interpolate(t.t().unsqueeze(0), size=span, mode="linear").squeeze(0).t()
+            return t.to(torch.float16).contiguous()
+        return fit(attn.rel_pos_h), fit(attn.rel_pos_w)
+
+    def buffers(self, b: int):
+        bufs = self._bufs.get(b)
+        if bufs is None:
+            g, c, dev = self.grid, self.C, self.device
+            hid = self.plans[0].lin1.outfeatures
+            assert all(p.lin1.outfeatures == hid for p in self.plans)
+            bufs = dict(
+                x=torch.empty((b, g, g, c), dtype=torch.float32, device=dev),
+                xn=torch.empty((b, g, g, c), dtype=torch.float16, device=dev),
+                qkv=torch.empty((b, g, g, 3 * c), dtype=torch.float16, device=dev),
+                att=torch.empty((b, g, g, c), dtype=torch.float16, device=dev),
+                hid=torch.empty((b, g, g, hid), dtype=torch.float16, device=dev),
+            )
+            self._bufs[b] = bufs
+        return bufs
+
+    # ---------------------------------------------------------------- stages
+    def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
+        b = img.shape[0]
+        p, g = self.patch, self.grid
+        cols = img.to(torch.float16).reshape(b, -1, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(b * g * g, -1)
+        y = torch.matmul(cols, self.pe_w.t()).float().view(b, g, g, -1)
+        if self.pe_b is not None:
+            y = y + self.pe_b
+        if self.pos is not None:
+            y = y + self.pos
+        x32.copy_(y)
+
+    def block(self, p: _BlockPlan, bufs) -> None:
+        x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
+        ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn)
+        p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
+        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
+        ops.layernorm(x, p.ln2_w, p.ln2_b, p.ln2_eps, out=xn)
+        p.lin1.forward_epilogue(xn, ops.EPI_BIAS_GELU, out=hid)
+        p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
+
+    def neck(self, x32: torch.Tensor, out_dtype) -> torch.Tensor:
+        b, g = x32.shape[0], self.grid
+        oc = self.out_chans
+        y = torch.matmul(x32.view(-1, self.C).to(torch.float16), self.n0_w.t())           # 1x1 conv
+        y = ops.layernorm(y.view(b, g, g, oc), *self.n1[:2], eps=self.n1[2])                # LN2d (NHWC rows)
+        cols = F.unfold(y.permute(0, 3, 1, 2), kernel_size=3, padding=1)                    # (b, oc*9, g*g)
+        y = torch.matmul(cols.transpose(1, 2), self.n2_w.t())                                # 3x3 conv
+        y = ops.layernorm(y.reshape(b, g, g, oc).contiguous(), *self.n3[:2], eps=self.n3[2],
+                          out_dtype=torch.float32)
+        return y.permute(0, 3, 1, 2).to(out_dtype)
+
+    # ---------------------------------------------------------------- forward
+    @torch.no_grad()
+    def forward(self, img: torch.Tensor, out_dtype=None) -> torch.Tensor:
+        assert img.is_cuda, "EncoderEngine runs on the GPU only"
+        b = img.shape[0]
+        bufs = self.buffers(b)
+        self.embed(img, bufs["x"])
+        for p in self.plans:
+            self.block(p, bufs)
+        return self.neck(bufs["x"], out_dtype or img.dtype)
+
+    __call__ = forward
+
+    @torch.no_grad()
+    def tokens(self, img: torch.Tensor, upto: int | None = None) -> torch.Tensor:
+        """fp32 residual stream after ``upto`` blocks (debug / parity helper)."""
+        bufs = self.buffers(img.shape[0])
+        self.embed(img, bufs["x"])
+        for p in self.plans[: (len(self.plans) if upto is None else upto)]:
+            self.block(p, bufs)
+        return bufs["x"].clone()
+
+    def capture(self, img_static: torch.Tensor, out_dtype=None):
+        """Record one forward on ``img_static`` into a HIP graph; returns ``(graph, out)``;
+        ``graph.replay()`` recomputes ``out`` from the current contents of ``img_static``."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.forward(img_static, out_dtype)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self.forward(img_static, out_dtype)
+        return graph, out

@@ -1,0 +1,119 @@
+"""``QuantLinear`` / ``make_quant`` / ``matmul4`` -- the reference's ``gptq_triton.quant_linear``
+API (``gptq_triton/quant_linear.py``) on the HIP W4A16 kernel.
+
+Same class/function names, constructor arguments, buffer names, dtypes and shapes as the
+reference (so a ``model.pt`` written by ``gptq4sam.py`` loads unchanged), same exceptions.
+Differences (documented in DESIGN.md):
+
+* no module-global ``workspace`` (reference ``:13``): outputs are fresh tensors, so calls are
+  reentrant, batch > 1 works and outputs never alias;
+* the weight is repacked ONCE into the kernel's fragment order (non-persistent buffer
+  ``wpacked``; rebuilt automatically if ``qweight`` changes);
+* shape constraints are relaxed to ``K % 64 == 0`` and ``N % 32 == 0``; the reference's
+  ``K != 8 * qweight.rows`` check still raises ``AssertionError``;
+* the bias add is fused into the GEMM epilogue.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+def make_quant(model: nn.Module, bits: int, groupsize: int) -> None:
+    """Replace every ``nn.Linear`` except one named ``lm_head`` by ``QuantLinear``
+    (reference ``quant_linear.py:15-36``)."""
+    for name, m in list(model.named_modules()):
+        if not isinstance(m, nn.Linear) or name == "lm_head":
+            continue
+        q = QuantLinear(bits, groupsize, m.in_features, m.out_features, m.bias is not None)
+        parent_name, _, child = name.rpartition(".")
+        parent = model.get_submodule(parent_name) if parent_name else model
+        setattr(parent, child, q)
+
+
+class QuantLinear(nn.Module):
+    """GPTQ int4 Linear (reference ``quant_linear.py:66-116``)."""
+
+    def __init__(self, bits: int, groupsize: int, infeatures: int, outfeatures: int, bias: bool):
+        super().__init__()
+        if bits not in [4]:
+            raise NotImplementedError("Only 4 bits are supported.")
+        groupsize = infeatures if groupsize == -1 else groupsize
+        self.infeatures = infeatures
+        self.outfeatures = outfeatures
+        self.bits = bits
+        self.groupsize = groupsize
+        per_int = 32 // bits
+        assert outfeatures % per_int == 0, "outfeatures must be a multiple of features_per_int"
+        ng = math.ceil(infeatures / groupsize)
+        self.register_buffer("qweight", torch.empty((infeatures // per_int, outfeatures), dtype=torch.int32))
+        self.register_buffer("qzeros", torch.empty((ng, outfeatures // per_int), dtype=torch.int32))
+        self.register_buffer("scales", torch.empty((ng, outfeatures), dtype=torch.float16))
+        if bias:
+            self.register_buffer("bias", torch.empty(outfeatures, dtype=torch.float16))
+        else:
+            self.register_parameter("bias", None)
+        self.register_buffer("wpacked", None, persistent=False)
+        self._packed_from = None
+
+    # -- kernel-side weight layout ------------------------------------------------------
+    def prepare(self) -> torch.Tensor:
+        """Repack ``qweight`` for the kernel (once; redone if the buffer was replaced)."""
+        key = (self.qweight.data_ptr(), self.qweight.device, self.qweight._version)
+        if self.wpacked is None or self._packed_from != key:
+            self.wpacked = ops.w4_repack(self.qweight)
+            self._packed_from = key
+        return self.wpacked
+
+    def forward_epilogue(self, x: torch.Tensor, epilogue: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        assert x.shape[-1] == self.qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
+        return ops.w4a16_gemm(x, self.prepare(), self.scales, self.qzeros, self.bias, self.outfeatures,
+                              self.groupsize, epilogue, out=out)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.forward_epilogue(x, ops.EPI_BIAS)
+
+    def extra_repr(self) -> str:
+        return f"infeatures={self.infeatures}, outfeatures={self.outfeatures}, bits={self.bits}, groupsize={self.groupsize}"
+
+
+def matmul4(groupsize: int, a: torch.Tensor, qweight: torch.Tensor, scales: torch.Tensor, qzeros: torch.Tensor,
+            bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Functional ``C = A x W4 + bias`` (reference ``triton_matmul4``, ``quant_linear.py:355-437``).
+
+    ``a`` (..., K) fp16; ``qweight`` int32 (K/8, N); ``scales`` fp16 (G, N); ``qzeros`` int32
+    (G, N/8); ``bias`` fp16 (N).  Returns a fresh fp16 (..., N).  The weight is repacked per
+    call (use ``QuantLinear`` to repack once).
+    """
+    assert a.shape[-1] == qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
+    k = a.shape[-1]
+    gs = -1 if groupsize in (-1, k) else groupsize
+    return ops.w4a16_gemm(a, ops.w4_repack(qweight), scales, qzeros,
+                          None if bias is None else bias.reshape(-1), qweight.shape[1], gs, ops.EPI_BIAS)
+
+
+# drop-in alias: the reference's name for the functional entry point
+triton_matmul4 = matmul4
+
+
+def autotune_warmup(model: nn.Module):
+    """Reference ``quant_linear.autotune_warmup`` (``:39-63``) returns per-(K,N) warmup closures.
+    There is no autotuner here (tile configs are chosen analytically); the closures repack the
+    weights and run one GEMM per unique shape so first-call costs leave the timed region."""
+    mods = [m for m in model.modules() if isinstance(m, QuantLinear)]
+    seen = {}
+    for m in mods:
+        seen.setdefault((m.infeatures, m.outfeatures), m)
+
+    def make(mod):
+        def run(mrows: int):
+            a = torch.randn(1, mrows, mod.infeatures, dtype=torch.float16, device=mod.qweight.device)
+            mod(a)
+        return run
+
+    return (make(m) for m in seen.values())

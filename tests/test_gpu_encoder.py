@@ -1,0 +1,79 @@
+"""Whole-encoder parity on the GPU (fused HIP engine) vs oracle G1 (fp32 CPU fake-quant path)
+and vs the reference's own golden encoder outputs.
+
+North-star tolerance (BASELINE.json): encoder output within 1e-2 max-abs of the reference
+fake-quant path.  Oracle G1 is pinned bit-exactly to the reference encoder at depth 2
+(test_oracle_golden.py) and the 32-block reference output is a committed fixture.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from _encoder_helpers import oracle_g1, oracle_vith, product_encoder
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-2
+
+
+def _report(name, out, ref):
+    d = np.abs(out - ref)
+    print(f"[parity] {name}: max-abs {d.max():.3e} mean-abs {d.mean():.3e} (ref absmax {np.abs(ref).max():.3f})")
+    return float(d.max())
+
+
+def test_vith_depth2_vs_reference_golden(cuda, golden_dir):
+    f = np.load(golden_dir / "encoder_vith2.npz", allow_pickle=False)
+    meta = json.loads(str(f["meta"]))
+    cfg, st, names, q = oracle_vith(2, meta["seed"], global_idx=(1,))
+    enc = product_encoder(cfg, st, names, q, -1, cuda)
+    img = torch.from_numpy(synth.make_images(1, seed=meta["image_seed"])).to(cuda)
+    out = enc.engine()(img, out_dtype=torch.float32).cpu().numpy()
+    err = _report("vit_h depth2 engine vs reference G1", out, f["out"])
+    assert err <= TOL
+    # module-by-module drop-in path (reference dataflow: fp16 model, per-module HIP ops)
+    enc.half()
+    with torch.no_grad():
+        out_m = enc.module_forward(img.half()).float().cpu().numpy()
+    err_m = _report("vit_h depth2 module path vs reference G1", out_m, f["out"])
+    assert err_m <= 2 * TOL
+
+
+@pytest.fixture(scope="module")
+def vith32(cuda, golden_dir):
+    f = np.load(golden_dir / "encoder_vith32.npz", allow_pickle=False)
+    meta = json.loads(str(f["meta"]))
+    cfg, st, names, q = oracle_vith(32, meta["seed"])
+    enc = product_encoder(cfg, st, names, q, -1, cuda)
+    img = synth.make_images(1, seed=meta["image_seed"])
+    return cfg, st, names, q, enc, img, f["out"].astype(np.float32)
+
+
+def test_vith32_vs_oracle_g1_and_reference_golden(cuda, vith32):
+    cfg, st, names, q, enc, img, golden16 = vith32
+    torch.set_num_threads(16)
+    ref = oracle_g1(cfg, st, names, q)(img).numpy()
+    assert np.abs(ref - golden16).max() < 3e-3  # golden stored in fp16
+    out = enc.engine()(torch.from_numpy(img).to(cuda), out_dtype=torch.float32).cpu().numpy()
+    err = _report("vit_h 32 blocks engine vs oracle G1", out, ref)
+    _report("vit_h 32 blocks engine vs reference golden (fp16-stored)", out, golden16)
+    assert err <= TOL
+
+
+def test_batch_and_graph_consistency(cuda, vith32):
+    *_, enc, img, _ = vith32
+    eng = enc.engine()
+    x1 = torch.from_numpy(img).to(cuda)
+    x2 = torch.cat([x1, torch.flip(x1, dims=[-1])])
+    y1 = eng(x1, out_dtype=torch.float32)
+    y2 = eng(x2, out_dtype=torch.float32)
+    assert (y2[:1] - y1).abs().max().item() < 1e-4
+    static = x2.clone()
+    graph, out = eng.capture(static, out_dtype=torch.float32)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert (out - y2).abs().max().item() == 0.0
+    assert torch.isfinite(out).all()

@@ -1,0 +1,192 @@
+"""GPU parity of the HIP kernels vs the CPU oracle (called through the C ABI).
+
+Tolerances (stated per test): fp16 outputs are compared at a few fp16 ulps of the output
+magnitude against an fp32 oracle fed the SAME fp16 inputs and the SAME packed int4 weights.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import gptq_pack, sam_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _packed_layer(k, n, groupsize, seed, zero_quirk=True):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    w = rng.standard_normal((n, k), dtype=np.float32) * np.float32(0.02)
+    if zero_quirk:
+        w[5] = np.abs(w[5])  # a zero point of 0 (quirk 4)
+    fake, s, z = gptq_pack.rtn_quantize_linear(w, groupsize)
+    qw, qz, sc = gptq_pack.pack_linear(fake, s, z, groupsize)
+    bias = (rng.standard_normal(n, dtype=np.float32) * np.float32(0.02)).astype(np.float16)
+    return qw, qz, sc, bias
+
+
+def _dev(a, cuda):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def _close(out, ref, rel):
+    out = out.float().cpu().numpy() if torch.is_tensor(out) else out
+    err = np.abs(out - ref).max()
+    scale = max(1.0, float(np.abs(ref).max()))
+    assert err <= rel * scale, f"max-abs {err:.3e} > {rel * scale:.3e}"
+    return err
+
+
+CFGS = [(1, 512), (2, 256), (3, 256), (4, 192), (5, 96), (6, 512)]
+
+
+@pytest.mark.parametrize("cfg,n", CFGS)
+@pytest.mark.parametrize("groupsize", [-1, 128])
+def test_w4a16_gemm_configs(cuda, cfg, n, groupsize):
+    from samq import ops
+    m, k = 333, 1280  # ragged M
+    qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=cfg * 7 + (groupsize > 0))
+    rng = np.random.Generator(np.random.PCG64(cfg))
+    a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+    ref = gptq_pack.matmul4_g1(a, qw, sc, qz, groupsize, bias)
+    packed = ops.w4_repack(_dev(qw, cuda))
+    out = ops.w4a16_gemm(_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, groupsize,
+                         ops.EPI_BIAS, cfg=cfg)
+    torch.cuda.synchronize()
+    # fp16 output rounding (2^-11 rel) + grouped fp16(q*s) weight rounding
+    _close(out, ref, 2e-3 if groupsize == -1 else 4e-3)
+
+
+@pytest.mark.parametrize("epi", ["gelu", "resadd", "f32"])
+def test_w4a16_gemm_epilogues(cuda, epi):
+    from samq import ops
+    m, k, n = 517, 2560, 768
+    qw, qz, sc, bias = _packed_layer(k, n, -1, seed=11)
+    rng = np.random.Generator(np.random.PCG64(12))
+    a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+    y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
+    packed = ops.w4_repack(_dev(qw, cuda))
+    args = (_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, -1)
+    if epi == "gelu":
+        ref = sam_ref.gelu_erf(torch.from_numpy(y)).numpy()
+        out = ops.w4a16_gemm(*args, ops.EPI_BIAS_GELU)
+        _close(out, ref, 2e-3)
+    elif epi == "resadd":
+        r0 = rng.standard_normal((m, n), dtype=np.float32)
+        res = _dev(r0, cuda)
+        ops.w4a16_gemm(*args, ops.EPI_RESADD_F32, out=res)
+        _close(res, r0 + y, 2e-5)
+    else:
+        out = ops.w4a16_gemm(*args, ops.EPI_F32)
+        _close(out, y, 2e-5)
+
+
+@pytest.mark.parametrize("tag", ["gm1", "g128"])
+def test_matmul4_functional_vs_reference_golden(cuda, golden_dir, tag):
+    """``triton_matmul4`` drop-in on the reference's own fixture: within fp16 rounding of the
+    fp32 fake-quant path (G1); the reference Triton output (G2) differs by its fp16 dequant."""
+    from samq import triton_matmul4
+    f = np.load(golden_dir / f"matmul4_{tag}.npz", allow_pickle=False)
+    g = int(f["groupsize"])
+    out = triton_matmul4(g, _dev(f["a"], cuda), _dev(f["qweight"], cuda), _dev(f["scales"], cuda),
+                         _dev(f["qzeros"], cuda), _dev(f["bias"], cuda)).float().cpu().numpy()
+    g1 = gptq_pack.matmul4_g1(f["a"], f["qweight"], f["scales"], f["qzeros"], g, f["bias"])
+    _close(out, g1, 2e-3)
+    assert np.abs(out - f["out"].astype(np.float32)).max() < 5e-3
+
+
+def test_matmul4_rejects_bad_k(cuda):
+    from samq import triton_matmul4
+    a = torch.zeros(4, 96, dtype=torch.float16, device=cuda)
+    with pytest.raises(AssertionError):
+        triton_matmul4(-1, a, torch.zeros(12, 64, dtype=torch.int32, device=cuda),
+                       torch.zeros(1, 64, dtype=torch.float16, device=cuda),
+                       torch.zeros(1, 8, dtype=torch.int32, device=cuda))
+    with pytest.raises(AssertionError):  # K != 8 * qweight rows
+        triton_matmul4(-1, torch.zeros(4, 128, dtype=torch.float16, device=cuda),
+                       torch.zeros(8, 64, dtype=torch.int32, device=cuda),
+                       torch.zeros(1, 64, dtype=torch.float16, device=cuda),
+                       torch.zeros(1, 8, dtype=torch.int32, device=cuda))
+
+
+@pytest.mark.parametrize("c", [256, 768, 1280])
+@pytest.mark.parametrize("in_dtype", [torch.float32, torch.float16])
+def test_layernorm(cuda, c, in_dtype):
+    from samq import ops
+    g = torch.Generator().manual_seed(c)
+    x = (torch.randn(1001, c, generator=g) * 3 + 1.5).to(in_dtype)
+    w = 1 + 0.1 * torch.randn(c, generator=g)
+    b = 0.1 * torch.randn(c, generator=g)
+    ref = torch.nn.functional.layer_norm(x.float(), (c,), w, b, eps=1e-6).numpy()
+    out = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6)
+    _close(out, ref, 1.5e-3)
+    out32 = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6, out_dtype=torch.float32)
+    _close(out32, ref, 2e-5)
+
+
+def _attn_case(b, h, w, heads, d, window, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    c = heads * d
+    x = rng.standard_normal((b, h, w, c), dtype=np.float32)
+    wq = rng.standard_normal((3 * c, c), dtype=np.float32) * np.float32(0.6 / math.sqrt(c))
+    bq = (rng.standard_normal(3 * c, dtype=np.float32) * np.float32(0.3)).astype(np.float16)
+    side = window if window else h
+    rph = (rng.standard_normal((2 * side - 1, d), dtype=np.float32) * np.float32(0.3)).astype(np.float16)
+    rpw = (rng.standard_normal((2 * side - 1, d), dtype=np.float32) * np.float32(0.3)).astype(np.float16)
+    # qkv as the GPU sees it (fp16); the oracle uses the same fp16 values
+    qkv16 = (x @ wq.T + bq.astype(np.float32)).astype(np.float16)
+    t = torch.from_numpy
+    if window:
+        # oracle: partition the LN output (zero pad) -> Linear -> pad tokens get exactly the bias
+        xw, pad_hw = sam_ref.window_partition(t(x), window)
+        qkvw = (xw @ t(wq).T + t(bq.astype(np.float32))).half().float()
+        o = sam_ref.attention_core(qkvw, heads, t(rph).float(), t(rpw).float())
+        ref = sam_ref.window_unpartition(o, window, pad_hw, (h, w)).numpy()
+    else:
+        ref = sam_ref.attention_core(t(qkv16).float(), heads, t(rph).float(), t(rpw).float()).numpy()
+    return qkv16, bq, rph, rpw, ref
+
+
+@pytest.mark.parametrize("b,h,w,heads,d,window", [
+    (2, 64, 64, 2, 80, 14),     # ViT-H windowed geometry (25 windows, pad 6)
+    (1, 20, 33, 3, 64, 14),     # ragged grid, vit_b head dim
+    (2, 64, 64, 2, 80, 0),      # ViT-H global
+    (1, 32, 32, 2, 64, 0),
+    (3, 16, 16, 2, 80, 0),
+    (2, 14, 14, 2, 80, 0),      # pre-partitioned window as a global 14x14 grid (QuantAttention module path)
+])
+def test_rel_attention(cuda, b, h, w, heads, d, window):
+    from samq import ops
+    qkv16, bq, rph, rpw, ref = _attn_case(b, h, w, heads, d, window, seed=h * 100 + w + d + window)
+    out = ops.rel_attention(_dev(qkv16, cuda), _dev(bq, cuda), _dev(rph, cuda), _dev(rpw, cuda), heads, window,
+                            d ** -0.5)
+    torch.cuda.synchronize()
+    # fp16 P (2^-11) and fp16 output rounding on |o| <~ 2
+    _close(out, ref, 2.5e-3)
+
+
+@pytest.mark.parametrize("tag", ["win", "glob"])
+def test_attention_functional_and_module_vs_reference_golden(cuda, golden_dir, tag):
+    import samq
+    from samq import fused_attention
+    f = np.load(golden_dir / f"attn_{tag}.npz", allow_pickle=False)
+    heads = int(f["heads"])
+    qkv = _dev(f["qkv"], cuda)
+    b, s = qkv.shape[0], qkv.shape[1]
+    d = qkv.shape[-1] // 3 // heads
+    q = qkv.reshape(b, s * s, 3, heads, d).permute(2, 0, 3, 1, 4).reshape(3, b * heads, s, s, d)[0]
+    rel_h, rel_w = fused_attention.add_decomposed_rel_pos(q, _dev(f["rel_pos_h"], cuda), _dev(f["rel_pos_w"], cuda),
+                                                          (s, s), (s, s))
+    o = fused_attention.forward(qkv, rel_h, rel_w, heads, d, d ** -0.5)
+    _close(o, f["attn_out"].astype(np.float32), 3e-3)
+    # module path: QuantAttention with fp16 nn.Linear projections, as the reference test builds it
+    c = heads * d
+    lq, lp = torch.nn.Linear(c, 3 * c).half().to(cuda), torch.nn.Linear(c, c).half().to(cuda)
+    with torch.no_grad():
+        lq.weight.copy_(_dev(f["wqkv"], cuda)); lq.bias.copy_(_dev(f["bqkv"], cuda))
+        lp.weight.copy_(_dev(f["wp"], cuda)); lp.bias.copy_(_dev(f["bp"], cuda))
+    qa = samq.QuantAttention(lq, lp, heads, d ** -0.5, True, torch.nn.Parameter(_dev(f["rel_pos_h"], cuda)),
+                             torch.nn.Parameter(_dev(f["rel_pos_w"], cuda)))
+    with torch.no_grad():
+        y = qa(_dev(f["x"], cuda))
+    _close(y, f["out"].astype(np.float32), 4e-3)

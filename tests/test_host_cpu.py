@@ -1,0 +1,130 @@
+"""Host-side logic on CPU: C-ABI exports, error mapping, product packer, module swaps,
+checkpoint round trip (no GPU compute)."""
+import ctypes
+import json
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from oracle import gptq_pack
+
+
+def test_library_exports_every_header_symbol():
+    from samq import _lib
+    lib = _lib.load()
+    header = (REPO / "include" / "samq.h").read_text()
+    decl = set(re.findall(r"^\s*(?:const char\*|int|size_t)\s+(samq_\w+)\s*\(", header, re.M))
+    assert decl, "no declarations parsed"
+    assert decl == set(_lib.SIGNATURES), (decl ^ set(_lib.SIGNATURES))
+    for name in decl:
+        assert getattr(lib, name) is not None
+    assert lib.samq_version() >= 100
+    assert lib.samq_w4_packed_words(1280, 3840) == 1280 * 3840 // 8
+
+
+def test_c_abi_rejects_bad_shapes_before_touching_the_device():
+    from samq import _lib
+    lib = _lib.load()
+    st = lib.samq_w4a16_gemm(ctypes.c_void_p(16), 96, ctypes.c_void_p(16), ctypes.c_void_p(16), ctypes.c_void_p(16),
+                             None, ctypes.c_void_p(16), 64, 8, 64, 96, -1, 0, None)
+    assert st == _lib.SAMQ_ERR_INVALID
+    assert "K must be a multiple of 64" in lib.samq_last_error().decode()
+    with pytest.raises(AssertionError):
+        _lib.check(st)
+    st = lib.samq_rel_attention(ctypes.c_void_p(16), None, ctypes.c_void_p(16), ctypes.c_void_p(16),
+                                ctypes.c_void_p(16), 1, 64, 64, 16, 96, 0, 0.1, None)
+    assert st == _lib.SAMQ_ERR_UNSUPPORTED
+    with pytest.raises(NotImplementedError):
+        _lib.check(st)
+
+
+@pytest.mark.parametrize("tag,g", [("gm1", -1), ("g128", 128)])
+def test_product_packer_bit_exact_vs_reference(golden_dir, tag, g):
+    from samq.gptq import pack_linear, rtn
+    from samq.quant_linear import QuantLinear
+    p = np.load(golden_dir / f"pack_{tag}.npz", allow_pickle=False)
+    w = torch.from_numpy(p["w"])
+    fake, s, z = rtn(w, g)
+    np.testing.assert_array_equal(s.numpy(), p["scale"])
+    np.testing.assert_array_equal(z.numpy(), p["zero"])
+    q = QuantLinear(4, g, 256, 128, True)
+    pack_linear(q, fake, s, z, torch.from_numpy(p["bias"]))
+    np.testing.assert_array_equal(q.qweight.numpy(), p["qweight"])
+    np.testing.assert_array_equal(q.qzeros.numpy(), p["qzeros"])
+    np.testing.assert_array_equal(q.scales.numpy(), p["scales"])
+    np.testing.assert_array_equal(q.bias.numpy(), p["bias16"])
+
+
+def test_quantlinear_buffers_match_reference_layout():
+    from samq import QuantLinear
+    q = QuantLinear(4, -1, 1280, 3840, True)
+    sd = q.state_dict()
+    assert set(sd) == {"qweight", "qzeros", "scales", "bias"}
+    assert sd["qweight"].shape == (160, 3840) and sd["qweight"].dtype == torch.int32
+    assert sd["qzeros"].shape == (1, 480) and sd["qzeros"].dtype == torch.int32
+    assert sd["scales"].shape == (1, 3840) and sd["scales"].dtype == torch.float16
+    q = QuantLinear(4, 128, 5120, 1280, False)
+    assert q.qzeros.shape == (40, 160) and q.bias is None
+    with pytest.raises(NotImplementedError):
+        QuantLinear(3, -1, 64, 64, True)
+
+
+def test_make_quant_and_attention_swap_and_load_quant_roundtrip(tmp_path):
+    import samq
+    from samq.gptq import quantize_rtn, save_quant
+    torch.manual_seed(0)
+    sam = samq.build_sam_vit_b(img_size=256)
+    enc = sam.image_encoder
+    n_lin = sum(isinstance(m, torch.nn.Linear) for m in enc.modules())
+    assert n_lin == 48
+    quantize_rtn(enc, groupsize=-1)
+    assert sum(isinstance(m, samq.QuantLinear) for m in enc.modules()) == 48
+    # zero one bias so load_quant drops it (reference __init__.py:57-61)
+    enc.blocks[0].mlp.lin1.bias.zero_()
+    save_quant(sam, tmp_path, 4, -1)
+    cfg = json.loads((tmp_path / "quant_config.json").read_text())
+    assert cfg == {"wbits": 4, "groupsize": -1}
+    sam2 = samq.build_sam_vit_b(img_size=256)
+    samq.load_quant(sam2, str(tmp_path), warmup_autotune=False, device=None, sub_module="image_encoder")
+    e2 = sam2.image_encoder
+    assert sum(isinstance(m, samq.QuantAttention) for m in e2.modules()) == 12
+    assert e2.blocks[0].mlp.lin1.bias is None
+    a, b = enc.state_dict(), sam2.state_dict()
+    for k, v in a.items():
+        kk = "image_encoder." + k.replace("attn.qkv.", "attn.qkv_proj.").replace("attn.proj.", "attn.o_proj.")
+        if k == "blocks.0.mlp.lin1.bias":
+            continue
+        assert torch.equal(v, b[kk]), k
+    with pytest.raises(FileNotFoundError):
+        (tmp_path / "model.pt").unlink()
+        samq.load_quant(samq.build_sam_vit_b(img_size=256), str(tmp_path), warmup_autotune=False, device=None,
+                        sub_module="image_encoder")
+
+
+def test_quantized_encoder_refuses_cpu():
+    import samq
+    from samq.gptq import quantize_rtn
+    enc = samq.build_sam_vit_b(img_size=256).image_encoder
+    quantize_rtn(enc)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        enc(torch.zeros(1, 3, 256, 256))
+
+
+def test_module_float_forward_matches_oracle():
+    """The host module tree (float, unquantized) == the oracle restatement (same weights)."""
+    import samq
+    from oracle import sam_ref, synth
+    cfg = synth.encoder_config("vit_b", img_size=256, depth=3, global_attn_indexes=(1,))
+    st = synth.make_encoder_state(cfg, seed=3)
+    enc = samq.ImageEncoderViT(img_size=256, embed_dim=768, depth=3, num_heads=12, mlp_ratio=4,
+                               norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6), use_rel_pos=True,
+                               global_attn_indexes=(1,), window_size=14)
+    enc.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    img = synth.make_images(1, 256, seed=4)
+    with torch.no_grad():
+        y = enc(torch.from_numpy(img)).numpy()
+    ref = sam_ref.EncoderOracle(cfg, st)(img).numpy()
+    assert np.abs(y - ref).max() < 1e-4
