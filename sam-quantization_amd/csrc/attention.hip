@@ -86,8 +86,10 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
   };
 
   // ---------------------------------------------------------------- Q fragments (scaled)
-  half8_t qf[QT][2];
-  half4_t qtail[QT];
+  // D = 80 is covered by three 16x16x32 k-steps; lanes of the third step with d >= D hold 0.
+  constexpr int KS = (D + 31) / 32;
+  const bool kin3 = 64 + 8 * g < D;   // lane group holds real d in the last k-step
+  half8_t qf[QT][KS];
   int qrow[QT], qcol0[QT];
   bool qvalid[QT];
 #pragma unroll
@@ -101,19 +103,12 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
     if (kind == 0) src = tok_ptr(qrow[t], qcol0[t] + ql) + head * D;
     else if (kind == 1 && p.qkv_bias) src = p.qkv_bias + head * D;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < KS; ++s) {
       half8_t v = {};
-      if (src) v = *(const half8_t*)(src + 32 * s + 8 * g);
+      if (src && (s < 2 || kin3)) v = *(const half8_t*)(src + 32 * s + 8 * g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * qscale);
       qf[t][s] = v;
-    }
-    if (D == 80) {
-      half4_t v = {};
-      if (src) v = *(const half4_t*)(src + 64 + 4 * g);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = (_Float16)((float)v[j] * qscale);
-      qtail[t] = v;
     }
   }
 
@@ -136,10 +131,11 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
           const _Float16* rp = tab + (int64_t)r * D;
           float4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const half8_t*)(rp + 32 * s + 8 * g), qf[t][s], a, 0, 0, 0);
-          if (D == 80)
-            a = __builtin_amdgcn_mfma_f32_16x16x16f16(*(const half4_t*)(rp + 64 + 4 * g), qtail[t], a, 0, 0, 0);
+          for (int s = 0; s < KS; ++s) {
+            half8_t ra = {};
+            if (s < 2 || kin3) ra = *(const half8_t*)(rp + 32 * s + 8 * g);
+            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(ra, qf[t][s], a, 0, 0, 0);
+          }
           a = a * inv_scale;
           if (which) {
             tw[t][kt] = a;
@@ -240,13 +236,13 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
       const char* krow = kb + ((kt * 16 + ql) * DP) * 2;
       const half8_t k0 = *(const half8_t*)(krow + (8 * g) * 2);
       const half8_t k1 = *(const half8_t*)(krow + (32 + 8 * g) * 2);
-      half4_t k2;
-      if (D == 80) k2 = *(const half4_t*)(krow + (64 + 4 * g) * 2);
+      half8_t k2 = {};
+      if (D == 80 && kin3) k2 = *(const half8_t*)(krow + (64 + 8 * g) * 2);
 #pragma unroll
       for (int t = 0; t < QT; ++t) {
         sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, qf[t][0], sc[t][kt], 0, 0, 0);
         sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, qf[t][1], sc[t][kt], 0, 0, 0);
-        if (D == 80) sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x16f16(k2, qtail[t], sc[t][kt], 0, 0, 0);
+        if (D == 80) sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k2, qf[t][KS - 1], sc[t][kt], 0, 0, 0);
       }
     }
 
