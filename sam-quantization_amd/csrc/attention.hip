@@ -7,26 +7,31 @@
 // are read from / written to the natural [B, H, W, C] layout, padded window tokens are
 // synthesised in-kernel (their q/k/v equal the qkv bias).
 //
-// Structure (gfx950, wave64, v_mfma_f32_16x16x{32,16}_f16):
+// Structure (gfx950, wave64, v_mfma_f32_16x16x32_f16, 7-8 waves per workgroup = 2 waves/SIMD):
 //  * work unit = (window or image, head, block of query tiles); a query tile is 16 queries of
-//    ONE grid row (grid rows are padded to SP = 16 or 64 slots), so every tile has a single
-//    query row index qh;
-//  * keys are consumed one GRID ROW at a time (SP slots): the scores of a key row are
+//    ONE grid row (rows padded to SP = 16 / 32 / 64 slots), so a tile has one query row qh;
+//  * keys are consumed one GRID ROW at a time (SP slots).  For key row kh the scores are
 //        s[q, kw] = q.k * scale + TH[q, kh] + TW[q, kw]
-//    where TW[q, kw] = q . Rw[qh - kw + S - 1] is the SAME for every key row, so it is computed
-//    once per query tile by MFMA straight into the score-tile register layout and used as the
-//    initial accumulator of every Q.K^T; TH[q, kh] = q . Rh[qh - kh + S - 1] is one scalar per
-//    (query, key row) kept in LDS.  (Both tables index the query ROW qh: reference quirk 1.)
-//  * scores are computed transposed (S^T = K . Q^T) so each lane owns one query and softmax
-//    row reductions are in-register + 2 cross-lane steps; P feeds P.V as the B operand with a
-//    permuted k order that V^T (staged transposed in LDS) reads with two ds_read_b64;
-//  * online softmax in exp2 domain, f32 statistics, f16 MFMA operands, f32 accumulation;
-//  * K / V^T key rows are register-prefetched and double-buffered in LDS (1 barrier / row).
+//    TW[q, kw] = q . Rw[qh - kw + S - 1] is identical for every key row: it is computed once per
+//    query tile by MFMA directly in the score-tile register layout and fed as the C input of
+//    every Q.K^T; TH[q, kh] = q . Rh[qh - kh + S - 1] is constant along the row, so it is folded
+//    into the running max instead of being added per score.  (Both tables are indexed by the
+//    query ROW qh: reference quirk 1.)
+//  * scores are computed transposed (S^T = K . Q^T): each lane owns one query, row reductions are
+//    in-register + 2 cross-lane steps; P feeds O^T += V^T . P^T as the B operand with a permuted
+//    k order that V^T supplies through ds_read_b64_tr_b16 from the row-major V tile;
+//  * K / V rows reach LDS by global_load_lds (no VGPR round trip): windows (S <= 16) are staged
+//    whole before the loop (no barrier inside it); global attention streams key rows through a
+//    3-deep LDS ring with counted vmcnt and one raw s_barrier per row;
+//  * online softmax in the exp2 domain with f32 statistics; the O rescale is skipped when no
+//    query of the wave raised its max (alpha == 1 exactly, bit-identical results).
 #include "common.h"
 
 namespace samq {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __attribute__((aligned(16))) _Float16 g_zero16[8];   // zero source for pad slots
 
 struct AttnParams {
   const _Float16* qkv;      // token stride tok_stride (elements); q at h*D, k at C+h*D, v at 2C+h*D
@@ -42,24 +47,33 @@ struct AttnParams {
   float scale;              // sm_scale
 };
 
-template <int D, int SP, int QT, bool PRECOMP>
-__global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
-  constexpr int KT = SP / 16;            // key tiles per key row
-  constexpr int DT = D / 16;             // d tiles
-  constexpr int DP = D + 8;              // K row pitch (halfs) in LDS
-  constexpr int VP = SP + 4;             // V^T row pitch (halfs)
-  constexpr int K_BYTES = SP * DP * 2;
-  constexpr int V_BYTES = D * VP * 2;
-  constexpr int BUF_BYTES = K_BYTES + V_BYTES;
-  constexpr int TH_BYTES = 4 * QT * SP * 16 * 4;
-  constexpr int D8 = D / 8;
-  constexpr int NCHUNK = 2 * SP * D8;
-  constexpr int CH = (NCHUNK + 255) / 256;
-  static_assert(D == 64 || D == 80, "head dim");
-  static_assert(SP == 16 || SP == 32 || SP == 64, "row pad");
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 15, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF_BYTES + TH_BYTES];
-  float* th_lds = (float*)(smem + 2 * BUF_BYTES);
+template <int D, int SP, int QT, int NW, bool RESIDENT, bool PRECOMP, int RS = 16>
+__global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p) {
+  constexpr int KT = SP / 16;                  // key tiles per key row
+  constexpr int DT = D / 16;                   // output d tiles
+  constexpr int KS = (D + 31) / 32;            // k32 steps of Q.K^T (D=80 -> 3, last half-zero)
+  constexpr int D8 = D / 8;                    // 16-byte chunks per token
+  constexpr int ROWB = SP * D * 2;             // bytes of one key row (K or V) in LDS
+  // RESIDENT: the keys of the whole (<= RS x RS) grid packed with row pitch S, plus 16 - S slack
+  // keys so the 16-slot tile of the last row stays in bounds (slots >= S are masked)
+  constexpr int RKEYS = RS * RS + 16 - RS;
+  constexpr int UNIT_CHUNKS = RESIDENT ? 2 * RKEYS * D8 : 2 * SP * D8;
+  constexpr int NI = (UNIT_CHUNKS + 64 * NW - 1) / (64 * NW);   // glds per wave per unit
+  constexpr int BUFB = NI * NW * 1024;
+  constexpr int NBUF = RESIDENT ? 1 : 3;
+  constexpr int TH_ROWS = RESIDENT ? 16 : SP;   // >= 16: the TH tile writes 16 rows
+  constexpr int TH_BYTES = NW * QT * TH_ROWS * 16 * 4;
+  static_assert(D == 64 || D == 80, "head dim");
+  static_assert(!RESIDENT || SP == 16, "resident mode holds <= 16 rows of 16 slots");
+
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUFB + TH_BYTES];
+  float* th_lds = (float*)(smem + NBUF * BUFB);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -76,7 +90,7 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
   const int C = p.C;
   const float qscale = p.scale * LOG2E;
 
-  // token helpers: 0 = real, 1 = window pad (bias), 2 = slot pad (masked / unused)
+  // 0 = real token, 1 = window pad (q/k/v = bias), 2 = slot beyond the row (masked / unused)
   auto tok_kind = [&](int y, int x) -> int {
     if (x >= S || y >= S) return 2;
     return (Y0 + y < p.H && X0 + x < p.W) ? 0 : 1;
@@ -85,20 +99,45 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
     return p.qkv + (((int64_t)b * p.H + (Y0 + y)) * p.W + (X0 + x)) * p.tok_stride;
   };
 
+  // ---------------------------------------------------------------- K/V staging (LDS-DMA)
+  // chunk c of a unit -> LDS byte c*16; unit layout [K|V][key][D] (STREAM: one row of SP slots;
+  // RESIDENT: key r*S + x of the whole grid)
+  auto issue = [&](int row0, int buf) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int c = (wave * NI + i) * 64 + lane;
+      const _Float16* src = g_zero16;
+      if (c < UNIT_CHUNKS) {
+        constexpr int HALF = UNIT_CHUNKS / 2;
+        const bool isv = c >= HALF;
+        const int cc = isv ? c - HALF : c;
+        const int key = cc / D8, d8 = cc % D8;
+        const int r = RESIDENT ? key / S : row0;
+        const int slot = RESIDENT ? key % S : key;
+        const int kind = r < S ? tok_kind(r, slot) : 2;
+        const int off = (isv ? 2 * C : C) + head * D + d8 * 8;
+        if (kind == 0) src = tok_ptr(r, slot) + off;
+        else if (kind == 1 && p.qkv_bias) src = p.qkv_bias + off;
+      }
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)src,
+                                       (SAMQ_LDS void*)(smem + buf * BUFB + (wave * NI + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  // start the K/V traffic first, it overlaps the Q / rel-pos prologue
+  issue(0, 0);
+  if (!RESIDENT && S > 1) issue(1, 1);
+
   // ---------------------------------------------------------------- Q fragments (scaled)
-  // D = 80 is covered by three 16x16x32 k-steps; lanes of the third step with d >= D hold 0.
-  constexpr int KS = (D + 31) / 32;
-  const bool kin3 = 64 + 8 * g < D;   // lane group holds real d in the last k-step
+  const bool kin3 = 64 + 8 * g < D;   // this lane group holds real d in the last k-step
   half8_t qf[QT][KS];
   int qrow[QT], qcol0[QT];
-  bool qvalid[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    const int qi = (blockIdx.x * 4 + wave) * QT + t;
+    const int qi = (blockIdx.x * NW + wave) * QT + t;
     qrow[t] = qi / KT;
     qcol0[t] = (qi % KT) * 16;
     const int kind = tok_kind(qrow[t], qcol0[t] + ql);
-    qvalid[t] = kind != 2;
     const _Float16* src = nullptr;
     if (kind == 0) src = tok_ptr(qrow[t], qcol0[t] + ql) + head * D;
     else if (kind == 1 && p.qkv_bias) src = p.qkv_bias + head * D;
@@ -115,7 +154,7 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
   // ---------------------------------------------------------------- rel-pos terms
   float4_t tw[QT][KT];
   const float inv_scale = 1.0f / p.scale;  // (Qs . R) / scale = log2e * (q . R)
-  float* th_w = th_lds + wave * (QT * SP * 16);
+  float* th_w = th_lds + wave * (QT * TH_ROWS * 16);
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     const int qh = qrow[t] < S ? qrow[t] : S - 1;
@@ -125,8 +164,7 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
         const _Float16* tab = which ? p.relw : p.relh;
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt) {
-          const int kk = kt * 16 + ql;                 // table row for the A operand
-          int r = qh - kk + S - 1;
+          int r = qh - (kt * 16 + ql) + S - 1;     // table row of this lane's A-operand row
           r = r < 0 ? 0 : r;
           const _Float16* rp = tab + (int64_t)r * D;
           float4_t a = {0.f, 0.f, 0.f, 0.f};
@@ -141,7 +179,7 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
             tw[t][kt] = a;
           } else {
 #pragma unroll
-            for (int r2 = 0; r2 < 4; ++r2) th_w[(t * SP + kt * 16 + 4 * g + r2) * 16 + ql] = a[r2];
+            for (int r2 = 0; r2 < 4; ++r2) th_w[(t * TH_ROWS + kt * 16 + 4 * g + r2) * 16 + ql] = a[r2];
           }
         }
       }
@@ -157,51 +195,11 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
           const int kk = kt * 16 + 4 * g + r2;
           const bool kin = ok && kk < S;
           tw[t][kt][r2] = kin ? (float)p.relw[base + kk] * LOG2E : 0.f;
-          th_w[(t * SP + kk) * 16 + ql] = kin ? (float)p.relh[base + kk] * LOG2E : 0.f;
+          th_w[(t * TH_ROWS + kk) * 16 + ql] = kin ? (float)p.relh[base + kk] * LOG2E : 0.f;
         }
       }
     }
   }
-
-  // ---------------------------------------------------------------- K/V staging
-  uint4 stg[CH];
-  auto load_row = [&](int kh) {
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int c = tid + 256 * i;
-      uint4 v = {0u, 0u, 0u, 0u};
-      if (c < NCHUNK) {
-        const bool isv = c >= SP * D8;
-        const int cc = isv ? c - SP * D8 : c;
-        const int x = cc / D8, d8 = cc % D8;
-        const int kind = tok_kind(kh, x);
-        const int off = (isv ? 2 * C : C) + head * D + d8 * 8;
-        if (kind == 0) v = *(const uint4*)(tok_ptr(kh, x) + off);
-        else if (kind == 1 && p.qkv_bias) v = *(const uint4*)(p.qkv_bias + off);
-      }
-      stg[i] = v;
-    }
-  };
-  auto store_row = [&](int buf) {
-    char* base = smem + buf * BUF_BYTES;
-    _Float16* vt = (_Float16*)(base + K_BYTES);
-#pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const int c = tid + 256 * i;
-      if (c < NCHUNK) {
-        const bool isv = c >= SP * D8;
-        const int cc = isv ? c - SP * D8 : c;
-        const int x = cc / D8, d8 = cc % D8;
-        if (!isv) {
-          *(uint4*)(base + (x * DP + d8 * 8) * 2) = stg[i];
-        } else {
-          const half8_t h = __builtin_bit_cast(half8_t, stg[i]);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) vt[(d8 * 8 + j) * VP + x] = h[j];
-        }
-      }
-    }
-  };
 
   float m[QT], l[QT];
   float4_t o[QT][DT];
@@ -212,46 +210,57 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
 #pragma unroll
     for (int d = 0; d < DT; ++d) o[t][d] = float4_t{0.f, 0.f, 0.f, 0.f};
   }
+  const bool mask_slots = S < SP;
+  const int trow = ql >> 2;            // ds_read_b64_tr_b16: lane 4q+p of a 16-lane group reads
+  const int tcol = 4 * (ql & 3);       // block row q, columns 4p..4p+3; receives column (lane&15)
 
-  load_row(0);
-  store_row(0);
-  __syncthreads();
+  if (RESIDENT) {
+    wait_vmcnt<0>();
+    __syncthreads();   // K/V of the whole window + TH visible
+  } else {
+    __syncthreads();   // TH visible (the K/V ring is ordered by counted vmcnt + s_barrier below)
+  }
 
   for (int kh = 0; kh < S; ++kh) {
-    const int buf = kh & 1;
-    if (kh + 1 < S) load_row(kh + 1);
-    const char* kb = smem + buf * BUF_BYTES;
-    const _Float16* vt = (const _Float16*)(kb + K_BYTES);
+    const char* kb;
+    if (RESIDENT) {
+      kb = smem + kh * S * (D * 2);
+    } else {
+      if (kh + 1 < S) wait_vmcnt<NI>(); else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();   // row kh landed for every wave; row kh-1 fully consumed
+      if (kh + 2 < S) issue(kh + 2, (kh + 2) % 3);
+      kb = smem + (kh % 3) * BUFB;
+    }
+    const char* vb = kb + (RESIDENT ? (UNIT_CHUNKS / 2) * 16 : ROWB);
 
-    // ---- scores S^T (per key tile, per query tile)
+    // ---- scores S^T = K . Q^T (+ TW as the C input)
     float4_t sc[QT][KT];
 #pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      const float thv = th_w[(t * SP + kh) * 16 + ql];
-#pragma unroll
-      for (int kt = 0; kt < KT; ++kt) sc[t][kt] = tw[t][kt] + thv;
-    }
-#pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
-      const char* krow = kb + ((kt * 16 + ql) * DP) * 2;
-      const half8_t k0 = *(const half8_t*)(krow + (8 * g) * 2);
-      const half8_t k1 = *(const half8_t*)(krow + (32 + 8 * g) * 2);
-      half8_t k2 = {};
-      if (D == 80 && kin3) k2 = *(const half8_t*)(krow + (64 + 8 * g) * 2);
+      const char* krow = kb + (kt * 16 + ql) * (D * 2);
+      half8_t kf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        kf[s] = half8_t{};
+        if (s < 2 || kin3) kf[s] = *(const half8_t*)(krow + (32 * s + 8 * g) * 2);
+      }
 #pragma unroll
       for (int t = 0; t < QT; ++t) {
-        sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k0, qf[t][0], sc[t][kt], 0, 0, 0);
-        sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k1, qf[t][1], sc[t][kt], 0, 0, 0);
-        if (D == 80) sc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(k2, qf[t][KS - 1], sc[t][kt], 0, 0, 0);
+        float4_t a = tw[t][kt];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[t][s], a, 0, 0, 0);
+        sc[t][kt] = a;
       }
     }
 
-    // ---- online softmax (exp2 domain)
+    // ---- online softmax (exp2 domain); TH[q, kh] is constant along the row
     half8_t pb[QT][(SP + 31) / 32];
     half4_t pb16[QT];
+    bool any_rescale = false;
+    float alpha[QT];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      if (SP > 14) {  // mask padded key slots (only when S < SP)
+      if (mask_slots) {
 #pragma unroll
         for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
@@ -261,25 +270,25 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
       float mx = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[t][kt][r]);
+        mx = fmaxf(fmaxf(mx, fmaxf(sc[t][kt][0], sc[t][kt][1])), fmaxf(sc[t][kt][2], sc[t][kt][3]));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m[t], mx);
-      const float alpha = __builtin_amdgcn_exp2f(m[t] - mnew);
+      const float th = th_w[(t * TH_ROWS + kh) * 16 + ql];
+      const float mnew = fmaxf(m[t], mx + th);
+      alpha[t] = __builtin_amdgcn_exp2f(m[t] - mnew);
+      any_rescale |= mnew != m[t];
       m[t] = mnew;
+      const float corr = mnew - th;
       float rs = 0.f;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __builtin_amdgcn_exp2f(sc[t][kt][r] - mnew);
+          const float e = __builtin_amdgcn_exp2f(sc[t][kt][r] - corr);
           sc[t][kt][r] = e;
           rs += e;
         }
-      l[t] = l[t] * alpha + rs;
-#pragma unroll
-      for (int d = 0; d < DT; ++d) o[t][d] = o[t][d] * alpha;
+      l[t] = l[t] * alpha[t] + rs;
       if (SP == 16) {
         pb16[t] = half4_t{(_Float16)sc[t][0][0], (_Float16)sc[t][0][1], (_Float16)sc[t][0][2], (_Float16)sc[t][0][3]};
       } else {
@@ -293,29 +302,35 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
         }
       }
     }
+    if (__any(any_rescale)) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+#pragma unroll
+        for (int d = 0; d < DT; ++d) o[t][d] = o[t][d] * alpha[t];
+    }
 
-    // ---- O^T += V^T . P^T
+    // ---- O^T += V^T . P^T  (V^T fragments by hardware-transposed LDS reads of row-major V)
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
-      const _Float16* vrow = vt + (d * 16 + ql) * VP;
       if (SP == 16) {
-        const half4_t va = *(const half4_t*)(vrow + 4 * g);
+        const char* a0 = vb + ((4 * g + trow) * D + d * 16 + tcol) * 2;
+        const half4_t va = __builtin_bit_cast(
+            half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0)));
 #pragma unroll
         for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x16f16(va, pb16[t], o[t][d], 0, 0, 0);
       } else {
 #pragma unroll
         for (int s = 0; s < SP / 32; ++s) {
-          const half4_t lo = *(const half4_t*)(vrow + 32 * s + 4 * g);
-          const half4_t hi = *(const half4_t*)(vrow + 32 * s + 16 + 4 * g);
+          const char* a0 = vb + ((32 * s + 4 * g + trow) * D + d * 16 + tcol) * 2;
+          const char* a1 = a0 + 16 * D * 2;
+          const half4_t lo = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0)));
+          const half4_t hi = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a1)));
           const half8_t va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
           for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][s], o[t][d], 0, 0, 0);
         }
       }
     }
-
-    if (kh + 1 < S) store_row(buf ^ 1);
-    __syncthreads();
   }
 
   // ---------------------------------------------------------------- normalise + store
@@ -325,7 +340,7 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
     const int x = qcol0[t] + ql;
-    if (!qvalid[t] || tok_kind(qrow[t], x) != 0) continue;
+    if (tok_kind(qrow[t], x) != 0) continue;
     const float inv = 1.0f / lt;
     _Float16* dst = p.out + (((int64_t)b * p.H + (Y0 + qrow[t])) * p.W + (X0 + x)) * C + head * D;
 #pragma unroll
@@ -338,11 +353,12 @@ __global__ __launch_bounds__(256) void rel_attention_kernel(AttnParams p) {
   }
 }
 
-template <int D, int SP, int QT, bool PRE>
+template <int D, int SP, int QT, int NW, bool RES, bool PRE, int RS = 16>
 static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
   const int tiles = p.S * (SP / 16);
-  const int qblocks = (tiles + 4 * QT - 1) / (4 * QT);
-  hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, PRE>), dim3(qblocks, p.heads, units), dim3(256), 0, stream, p);
+  const int qblocks = (tiles + NW * QT - 1) / (NW * QT);
+  hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS>), dim3(qblocks, p.heads, units), dim3(64 * NW), 0,
+                     stream, p);
   SAMQ_LAUNCH_CHECK("rel_attention launch");
   return SAMQ_OK;
 }
@@ -350,12 +366,18 @@ static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
 template <bool PRE>
 static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t stream) {
   const int S = p.S;
-  if (S <= 16) {
-    return hd == 80 ? launch_attn<80, 16, 4, PRE>(p, units, stream) : launch_attn<64, 16, 4, PRE>(p, units, stream);
+  if (S <= 16) {  // whole window / small grid resident in LDS; one query tile per grid row
+    if (S == 14)
+      return hd == 80 ? launch_attn<80, 16, 2, 7, true, PRE, 14>(p, units, stream)
+                      : launch_attn<64, 16, 2, 7, true, PRE, 14>(p, units, stream);
+    return hd == 80 ? launch_attn<80, 16, 2, 8, true, PRE>(p, units, stream)
+                    : launch_attn<64, 16, 2, 8, true, PRE>(p, units, stream);
   } else if (S == 32) {
-    return hd == 80 ? launch_attn<80, 32, 2, PRE>(p, units, stream) : launch_attn<64, 32, 2, PRE>(p, units, stream);
+    return hd == 80 ? launch_attn<80, 32, 2, 8, false, PRE>(p, units, stream)
+                    : launch_attn<64, 32, 2, 8, false, PRE>(p, units, stream);
   } else {
-    return hd == 80 ? launch_attn<80, 64, 2, PRE>(p, units, stream) : launch_attn<64, 64, 2, PRE>(p, units, stream);
+    return hd == 80 ? launch_attn<80, 64, 2, 8, false, PRE>(p, units, stream)
+                    : launch_attn<64, 64, 2, 8, false, PRE>(p, units, stream);
   }
 }
 
@@ -391,8 +413,8 @@ extern "C" int samq_rel_attention(const void* qkv, const void* qkv_bias, const v
     units = B * p.upi;
   } else {
     SAMQ_REQUIRE(H == W, SAMQ_ERR_UNSUPPORTED, "rel_attention: global attention needs H == W");
-    SAMQ_REQUIRE(H == 16 || H == 32 || H == 64 || H < 16, SAMQ_ERR_UNSUPPORTED,
-                 "rel_attention: global grid side must be < 16, 16, 32 or 64");
+    SAMQ_REQUIRE(H <= 16 || H == 32 || H == 64, SAMQ_ERR_UNSUPPORTED,
+                 "rel_attention: global grid side must be <= 16, 32 or 64");
     p.S = H;
     p.nwx = 1;
     p.upi = 1;

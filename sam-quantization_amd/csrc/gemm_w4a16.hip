@@ -57,7 +57,7 @@ __global__ void w4_repack_kernel(const uint32_t* __restrict__ qweight, uint32_t*
 }
 
 // ------------------------------------------------------------------ GEMM
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED, int VAR = 1>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
                        const u32x4* __restrict__ Wp,
@@ -165,6 +165,11 @@ void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
   }
   const int hsel = lane >> 5;
 
+  // unpack constants held in VGPRs (opaque to the compiler) so (x & M) | MAGIC fuses into one
+  // v_and_or_b32 (gfx950 VOP3 takes no literal operands)
+  uint32_t kMask = 0x000F000Fu, kMagic = 0x64006400u;
+  if (VAR & 1) asm volatile("" : "+v"(kMask), "+v"(kMagic));
+
   // prologue
   stage_a(0, 0);
   u32x4 bcur[TN], bnext[TN];
@@ -201,7 +206,7 @@ void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
         half8_t bf;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t bits = ((w >> (4 * i)) & 0x000F000Fu) | 0x64006400u;
+          const uint32_t bits = ((w >> (4 * i)) & kMask) | kMagic;
           half2_t h = __builtin_bit_cast(half2_t, bits) - zc[t];
           if (GROUPED) h = h * sc[t];
           bf[2 * i] = h[0];
@@ -249,45 +254,265 @@ void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
   }
 }
 
+// ------------------------------------------------------------------ GEMM v3 (3-stage LDS-DMA ring)
+// Both operands reach LDS by global_load_lds: A (BM rows x 128 B, XOR-swizzled through the
+// source address) and B (BN/32 packed 1-KiB fragment blocks, already in lane order); a 3-slot
+// ring keeps two K tiles in flight behind counted vmcnt waits and ONE raw s_barrier per K tile
+// (no vmcnt(0) drain in the loop).  Fragment reads: A ds_read_b128 (conflict-free swizzle),
+// B ds_read_b128 lane-linear.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N <= 15, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED, int VAR = 0>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
+void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
+                   const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
+                   const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
+                   int M, int N, int K, int groupsize) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M;
+  constexpr int WN = BN / WAVES_N;
+  constexpr int TM = WM / 32;
+  constexpr int TN = WN / 32;
+  constexpr int BK = 64;
+  constexpr int ROWB = BK * 2;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int NA = BM / 8;                 // A pieces (1 KiB = 8 rows) per stage
+  constexpr int NB = BN / 32;                // B pieces (one packed n-tile block) per stage
+  constexpr int NT = NA + NB;
+  constexpr int NPW = (NT + NW - 1) / NW;    // glds per wave per stage
+  constexpr int STAGE = A_BYTES + NB * 1024;
+  constexpr int STAGES = 3;
+  static_assert(TM >= 1 && TN >= 1 && NPW <= 15, "bad tile");
+
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = K / BK;
+
+  // ---- this wave's LDS-DMA pieces: global source (per lane) and LDS offset (wave-uniform)
+  const char* src[NPW];
+  int dst[NPW];
+  int64_t step[NPW];   // source advance per K tile (bytes)
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    int j = wave * NPW + i;
+    j = j < NT ? j : NT - 1;   // surplus slots re-issue the last piece (same bytes, same place)
+    if (j < NA) {
+      const int row = j * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      src[i] = (const char*)(A + (int64_t)gr * lda + c * 8);
+      dst[i] = j * 1024;
+      step[i] = BK * 2;
+    } else {
+      const int nt = n0 / 32 + (j - NA);
+      src[i] = (const char*)(Wp + ((int64_t)nt * kt_count) * 64 + lane);
+      dst[i] = A_BYTES + (j - NA) * 1024;
+      step[i] = 64 * 16;
+    }
+  }
+  auto issue = [&](int kt, int slot) {
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + kt * step[i]),
+                                       (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+  };
+
+  int col[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+  half2_t zc[TN], sc[TN];
+  auto load_zc = [&](int g) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const uint32_t zw = qzeros[(int64_t)g * (N / 8) + (col[t] >> 3)];
+      const _Float16 z = (_Float16)(1024 + (int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
+      zc[t] = half2_t{z, z};
+      if (GROUPED) {
+        const _Float16 s = scales[(int64_t)g * N + col[t]];
+        sc[t] = half2_t{s, s};
+      }
+    }
+  };
+  load_zc(0);
+  int cur_group = 0;
+
+  uint32_t kMask = 0x000F000Fu, kMagic = 0x64006400u;
+  asm volatile("" : "+v"(kMask), "+v"(kMagic));
+
+  float16_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  int a_off[TM], a_swz[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_off[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
+  }
+  const int hsel = lane >> 5;
+
+  issue(0, 0);
+  if (kt_count > 1) issue(1, 1);
+  int slot = 0;
+  for (int kt = 0; kt < kt_count; ++kt) {
+    if (kt + 1 < kt_count) vm_wait<NPW>(); else vm_wait<0>();
+    __builtin_amdgcn_s_barrier();          // tile kt visible to all; slot (kt+2)%3 free
+    if (kt + 2 < kt_count) {
+      int s2 = slot + 2;
+      s2 = s2 >= STAGES ? s2 - STAGES : s2;
+      issue(kt + 2, s2);
+    }
+    if (GROUPED) {
+      const int g = (kt * BK) / groupsize;
+      if (g != cur_group) { load_zc(g); cur_group = g; }
+    }
+    const char* abase = smem + slot * STAGE;
+    u32x4 bw[TN];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) bw[t] = *(const u32x4*)(abase + A_BYTES + (wn * TN + t) * 1024 + lane * 16);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      half8_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const half8_t*)(abase + a_off[i] + (((2 * s + hsel) ^ a_swz[i]) << 4));
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const uint32_t w = bw[t][s];
+        half8_t bf;
+        if (VAR == 1) {   // TIMING-ONLY variant (wrong results): MFMA on the raw words, no unpack
+          bf = __builtin_bit_cast(half8_t, bw[t]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            half2_t h = __builtin_bit_cast(half2_t, ((w >> (4 * i)) & kMask) | kMagic) - zc[t];
+            if (GROUPED) h = h * sc[t];
+            bf[2 * i] = h[0];
+            bf[2 * i + 1] = h[1];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf, acc[i][t], 0, 0, 0);
+      }
+    }
+    slot = slot + 1 == STAGES ? 0 : slot + 1;
+  }
+
+  // ---- epilogue: y = acc * s[n] + b[n] -> GELU / residual / store
+  float csc[TN], cb[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    csc[t] = GROUPED ? 1.0f : (float)scales[col[t]];
+    cb[t] = bias ? (float)bias[col[t]] : 0.0f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+      if (row >= M) continue;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        float v = acc[i][t][r] * csc[t] + cb[t];
+        if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast(v);
+        if (EPI == SAMQ_EPI_RESADD_F32) {
+          float* cp = (float*)Cout + (int64_t)row * ldc + col[t];
+          *cp = *cp + v;
+        } else if (EPI == SAMQ_EPI_F32) {
+          ((float*)Cout)[(int64_t)row * ldc + col[t]] = v;
+        } else {
+          ((_Float16*)Cout)[(int64_t)row * ldc + col[t]] = (_Float16)v;
+        }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 struct GemmArgs {
   const _Float16* A; int64_t lda; const u32x4* Wp; const _Float16* scales; const uint32_t* qzeros;
   const _Float16* bias; void* C; int64_t ldc; int M, N, K, groupsize;
 };
 
-template <int BM, int BN, int WMW, int WNW, int EPI, bool GR>
+template <int BM, int BN, int WMW, int WNW, int EPI, bool GR, int VAR = 1>
 static int launch_cfg(const GemmArgs& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
-  hipLaunchKernelGGL((w4a16_gemm_kernel<BM, BN, WMW, WNW, EPI, GR>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+  hipLaunchKernelGGL((w4a16_gemm_kernel<BM, BN, WMW, WNW, EPI, GR, VAR>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
                      a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize);
   SAMQ_LAUNCH_CHECK("w4a16_gemm launch");
+  return SAMQ_OK;
+}
+
+template <int BM, int BN, int WMW, int WNW, int EPI, bool GR, int VAR = 0>
+static int launch_v3(const GemmArgs& a, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  hipLaunchKernelGGL((w4a16_gemm_v3<BM, BN, WMW, WNW, EPI, GR, VAR>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize);
+  SAMQ_LAUNCH_CHECK("w4a16_gemm_v3 launch");
   return SAMQ_OK;
 }
 
 template <int EPI, bool GR>
 static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
   switch (cfg) {
+    case 21: return launch_v3<256, 256, 2, 4, EPI, GR>(a, st);
+    case 22: return launch_v3<128, 256, 2, 4, EPI, GR>(a, st);
+    case 23: return launch_v3<128, 128, 2, 2, EPI, GR>(a, st);
+    case 24: return launch_v3<256, 128, 2, 2, EPI, GR>(a, st);
+    case 25: return launch_v3<128, 256, 1, 4, EPI, GR>(a, st);
+    case 26: return launch_v3<64, 64, 2, 2, EPI, GR>(a, st);
+    case 27: return launch_v3<128, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
+    case 28: return launch_v3<256, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
     case 1: return launch_cfg<256, 256, 2, 4, EPI, GR>(a, st);
     case 2: return launch_cfg<256, 128, 2, 2, EPI, GR>(a, st);
     case 3: return launch_cfg<128, 128, 2, 2, EPI, GR>(a, st);
     case 4: return launch_cfg<64, 64, 2, 2, EPI, GR>(a, st);
     case 5: return launch_cfg<64, 32, 2, 1, EPI, GR>(a, st);
     case 6: return launch_cfg<128, 256, 1, 4, EPI, GR>(a, st);
+    case 7: return launch_cfg<256, 256, 1, 8, EPI, GR>(a, st);
+    case 8: return launch_cfg<256, 128, 1, 4, EPI, GR>(a, st);
+    case 9: return launch_cfg<128, 256, 2, 4, EPI, GR>(a, st);
+    case 11: return launch_cfg<256, 256, 2, 4, EPI, GR, 0>(a, st);   // literal-constant unpack (A/B)
     default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown tile config");
   }
 }
 
+// Measured on MI355X (tools/bench_gemm.py, ViT-H shapes at M = 16384): the 3-stage LDS-DMA
+// kernel with 128x256 tiles / 64x64 wave tiles (cfg 22, 2 workgroups per CU) is the fastest or
+// within 2 % of it on every projection shape and beats dense fp16 hipBLASLt on 3 of 4.
 static int pick_cfg(int M, int N) {
-  if (N % 256 == 0 && M >= 4096) return 1;
-  if (N % 128 == 0 && M >= 2048) return 2;
-  if (N % 128 == 0) return 3;
-  if (N % 64 == 0) return 4;
+  if (N % 256 == 0 && M >= 1024) return 22;
+  if (N % 128 == 0 && M >= 512) return 23;
+  if (N % 64 == 0) return 26;
   return 5;
 }
 
 static int cfg_bn(int cfg) {
   switch (cfg) { case 1: return 256; case 2: return 128; case 3: return 128; case 4: return 64;
-                 case 5: return 32; case 6: return 256; default: return 0; }
+                 case 5: return 32; case 6: return 256; case 7: return 256; case 8: return 128;
+                 case 9: return 256; case 11: return 256; case 21: return 256; case 22: return 256;
+                 case 23: return 128; case 24: return 128; case 25: return 256; case 26: return 64;
+                 case 27: return 256; case 28: return 256;
+                 default: return 0; }
 }
 
 }  // namespace samq

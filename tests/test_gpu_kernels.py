@@ -37,7 +37,8 @@ def _close(out, ref, rel):
     return err
 
 
-CFGS = [(1, 512), (2, 256), (3, 256), (4, 192), (5, 96), (6, 512)]
+CFGS = [(1, 512), (2, 256), (3, 256), (4, 192), (5, 96), (6, 512), (7, 512), (9, 512), (21, 512), (22, 512),
+        (23, 256), (24, 256), (25, 512), (26, 192)]
 
 
 @pytest.mark.parametrize("cfg,n", CFGS)
