@@ -55,6 +55,11 @@ size_t samq_w4_packed_words(int K, int N);
  * by load_quant (replaces the reference's per-call B-tile addressing, quant_linear.py:292-294). */
 int samq_w4_repack(const int32_t* qweight, int32_t* packed, int K, int N, hipStream_t stream);
 
+/* Same with an explicit fragment layout (1: 32x32x16 MFMA order, 2: 16x16x32 order); for the
+ * tuning entry point samq_w4a16_gemm_cfg (cfg >= 40 expects layout 2, others layout 1). */
+int samq_w4_repack_layout(const int32_t* qweight, int32_t* packed, int K, int N, int layout,
+                          hipStream_t stream);
+
 /* C = epilogue(A[M,K] (f16, row stride lda) x W4[K,N]).  Replaces triton_matmul4 +
  * matmul4_kernel (gptq_triton/quant_linear.py:355-437, 231-352) and the separate `c + bias`
  * (:434-435).  wpacked from samq_w4_repack; scales f16 (G,N); qzeros int32 (G,N/8);

@@ -53,7 +53,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int D, int SP, int QT, int NW, bool RESIDENT, bool PRECOMP, int RS = 16>
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  // one v_max3_f32; fmaxf on MFMA results otherwise gets canonicalising v_max copies
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+template <int D, int SP, int QT, int NW, bool RESIDENT, bool PRECOMP, int RS = 16, int SC = 0>
 __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p) {
   constexpr int KT = SP / 16;                  // key tiles per key row
   constexpr int DT = D / 16;                   // output d tiles
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   const int g = lane >> 4;
   const int head = blockIdx.y;
   const int unit = blockIdx.z;
-  const int S = p.S;
+  const int S = SC ? SC : p.S;   // grid side, compile-time where the dispatcher knows it
   const int b = unit / p.upi;
   const int wi = unit % p.upi;
   const int Y0 = (wi / p.nwx) * S;
@@ -102,23 +109,35 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   // ---------------------------------------------------------------- K/V staging (LDS-DMA)
   // chunk c of a unit -> LDS byte c*16; unit layout [K|V][key][D] (STREAM: one row of SP slots;
   // RESIDENT: key r*S + x of the whole grid)
+  // per-lane sources for key row 0 (STREAM) / the whole grid (RESIDENT); a STREAM row kh is the
+  // same pattern kh grid rows further down, so the loop only adds kh * rowstride
+  const _Float16* src0[NI];
+  bool adv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = (wave * NI + i) * 64 + lane;
+    const _Float16* src = g_zero16;
+    bool real = false;
+    if (c < UNIT_CHUNKS) {
+      constexpr int HALF = UNIT_CHUNKS / 2;
+      const bool isv = c >= HALF;
+      const int cc = isv ? c - HALF : c;
+      const int key = cc / D8, d8 = cc % D8;
+      const int r = RESIDENT ? key / S : 0;
+      const int slot = RESIDENT ? key % S : key;
+      const int kind = r < S ? tok_kind(r, slot) : 2;
+      const int off = (isv ? 2 * C : C) + head * D + d8 * 8;
+      if (kind == 0) { src = tok_ptr(r, slot) + off; real = true; }
+      else if (kind == 1 && p.qkv_bias) src = p.qkv_bias + off;
+    }
+    src0[i] = src;
+    adv[i] = real && !RESIDENT;
+  }
+  const int64_t rowstride = (int64_t)p.W * p.tok_stride;
   auto issue = [&](int row0, int buf) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int c = (wave * NI + i) * 64 + lane;
-      const _Float16* src = g_zero16;
-      if (c < UNIT_CHUNKS) {
-        constexpr int HALF = UNIT_CHUNKS / 2;
-        const bool isv = c >= HALF;
-        const int cc = isv ? c - HALF : c;
-        const int key = cc / D8, d8 = cc % D8;
-        const int r = RESIDENT ? key / S : row0;
-        const int slot = RESIDENT ? key % S : key;
-        const int kind = r < S ? tok_kind(r, slot) : 2;
-        const int off = (isv ? 2 * C : C) + head * D + d8 * 8;
-        if (kind == 0) src = tok_ptr(r, slot) + off;
-        else if (kind == 1 && p.qkv_bias) src = p.qkv_bias + off;
-      }
+      const _Float16* src = adv[i] ? src0[i] + row0 * rowstride : src0[i];
       __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)src,
                                        (SAMQ_LDS void*)(smem + buf * BUFB + (wave * NI + i) * 1024), 16, 0, 0);
     }
@@ -267,12 +286,15 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
           for (int r = 0; r < 4; ++r)
             if (kt * 16 + 4 * g + r >= S) sc[t][kt][r] = -INFINITY;
       }
-      float mx = -INFINITY;
+      float mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
+      mx = max3f(mx, sc[t][0][3], mx);
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt)
-        mx = fmaxf(fmaxf(mx, fmaxf(sc[t][kt][0], sc[t][kt][1])), fmaxf(sc[t][kt][2], sc[t][kt][3]));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int kt = 1; kt < KT; ++kt) {
+        mx = max3f(mx, sc[t][kt][0], sc[t][kt][1]);
+        mx = max3f(mx, sc[t][kt][2], sc[t][kt][3]);
+      }
+      mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
+      mx = max3f(mx, __shfl_xor(mx, 16, 64), mx);
       const float th = th_w[(t * TH_ROWS + kh) * 16 + ql];
       const float mnew = fmaxf(m[t], mx + th);
       alpha[t] = __builtin_amdgcn_exp2f(m[t] - mnew);
@@ -353,12 +375,12 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   }
 }
 
-template <int D, int SP, int QT, int NW, bool RES, bool PRE, int RS = 16>
+template <int D, int SP, int QT, int NW, bool RES, bool PRE, int RS = 16, int SC = 0>
 static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
   const int tiles = p.S * (SP / 16);
   const int qblocks = (tiles + NW * QT - 1) / (NW * QT);
-  hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS>), dim3(qblocks, p.heads, units), dim3(64 * NW), 0,
-                     stream, p);
+  hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS, SC>), dim3(qblocks, p.heads, units),
+                     dim3(64 * NW), 0, stream, p);
   SAMQ_LAUNCH_CHECK("rel_attention launch");
   return SAMQ_OK;
 }
@@ -368,16 +390,16 @@ static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t str
   const int S = p.S;
   if (S <= 16) {  // whole window / small grid resident in LDS; one query tile per grid row
     if (S == 14)
-      return hd == 80 ? launch_attn<80, 16, 2, 7, true, PRE, 14>(p, units, stream)
-                      : launch_attn<64, 16, 2, 7, true, PRE, 14>(p, units, stream);
+      return hd == 80 ? launch_attn<80, 16, 2, 7, true, PRE, 14, 14>(p, units, stream)
+                      : launch_attn<64, 16, 2, 7, true, PRE, 14, 14>(p, units, stream);
     return hd == 80 ? launch_attn<80, 16, 2, 8, true, PRE>(p, units, stream)
                     : launch_attn<64, 16, 2, 8, true, PRE>(p, units, stream);
   } else if (S == 32) {
-    return hd == 80 ? launch_attn<80, 32, 2, 8, false, PRE>(p, units, stream)
-                    : launch_attn<64, 32, 2, 8, false, PRE>(p, units, stream);
+    return hd == 80 ? launch_attn<80, 32, 2, 8, false, PRE, 16, 32>(p, units, stream)
+                    : launch_attn<64, 32, 2, 8, false, PRE, 16, 32>(p, units, stream);
   } else {
-    return hd == 80 ? launch_attn<80, 64, 2, 8, false, PRE>(p, units, stream)
-                    : launch_attn<64, 64, 2, 8, false, PRE>(p, units, stream);
+    return hd == 80 ? launch_attn<80, 64, 2, 8, false, PRE, 16, 64>(p, units, stream)
+                    : launch_attn<64, 64, 2, 8, false, PRE, 16, 64>(p, units, stream);
   }
 }
 

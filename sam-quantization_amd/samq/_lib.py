@@ -36,6 +36,7 @@ SIGNATURES = {
     "samq_version": (_i32, []),
     "samq_w4_packed_words": (ctypes.c_size_t, [_i32, _i32]),
     "samq_w4_repack": (_i32, [_vp, _vp, _i32, _i32, _vp]),
+    "samq_w4_repack_layout": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),

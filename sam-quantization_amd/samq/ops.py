@@ -32,13 +32,19 @@ def _need_cuda(*ts):
 
 
 # ----------------------------------------------------------------------------- W4A16
-def w4_repack(qweight: torch.Tensor) -> torch.Tensor:
-    """Reference ``qweight`` int32 (K/8, N) -> kernel fragment layout (flat int32 K*N/8)."""
+def w4_repack(qweight: torch.Tensor, layout: int = 0) -> torch.Tensor:
+    """Reference ``qweight`` int32 (K/8, N) -> kernel fragment layout (flat int32 K*N/8).
+    ``layout`` 0 = the product layout expected by the default GEMM dispatch."""
     _need_cuda(qweight)
     assert qweight.dtype == torch.int32 and qweight.dim() == 2
     k, n = qweight.shape[0] * 8, qweight.shape[1]
     out = torch.empty(k * n // 8, dtype=torch.int32, device=qweight.device)
-    _lib.check(_lib.load().samq_w4_repack(_ptr(qweight.contiguous()), _ptr(out), k, n, _stream()), "w4_repack")
+    lib = _lib.load()
+    if layout:
+        st = lib.samq_w4_repack_layout(_ptr(qweight.contiguous()), _ptr(out), k, n, layout, _stream())
+    else:
+        st = lib.samq_w4_repack(_ptr(qweight.contiguous()), _ptr(out), k, n, _stream())
+    _lib.check(st, "w4_repack")
     return out
 
 

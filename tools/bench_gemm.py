@@ -44,13 +44,15 @@ def main():
         fake, s, z = rtn(w)
         pack_linear(q, fake, s, z, torch.randn(n, device=dev) * 0.02)
         packed = q.prepare()
+        packed2 = ops.w4_repack(q.qweight, layout=2)
+        pk = lambda c: packed2 if c >= 40 else packed  # noqa: E731
         a = torch.randn(m, k, device=dev).half()
         f32 = epi in (ops.EPI_RESADD_F32, ops.EPI_F32)
         outs = {}
         for c in cfgs + [3]:
             out = torch.zeros(m, n, device=dev, dtype=torch.float32 if f32 else torch.float16)
             try:
-                ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=out, cfg=c)
+                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=out, cfg=c)
             except AssertionError as e:
                 print(f"{name} cfg {c}: skipped ({e})")
                 continue
@@ -62,10 +64,10 @@ def main():
         for _ in range(3):
             for c in outs:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
+                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
                 e0.record(stream)
                 for _ in range(args.iters):
-                    ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
+                    ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[c].append(e0.elapsed_time(e1) / args.iters * 1e3)
@@ -74,7 +76,7 @@ def main():
             us = min(times[c])
             # residual epilogues accumulate: compare a fresh single launch instead
             o = torch.zeros_like(outs[c])
-            ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=o, cfg=c)
+            ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=o, cfg=c)
             r = torch.zeros_like(outs[3])
             ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=r, cfg=3)
             err = (o.float() - r.float()).abs().max().item()
