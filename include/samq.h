@@ -39,6 +39,11 @@ extern "C" {
 #define SAMQ_EPI_BIAS_GELU 1   /* C f16  = GELU_erf(y)              (MLPBlock lin1 + act)     */
 #define SAMQ_EPI_RESADD_F32 2  /* C f32 += y (in place)             (Block residual adds)     */
 #define SAMQ_EPI_F32 3         /* C f32  = y                                                  */
+/* int8-activation GEMMs only (samq_w8a8_gemm / samq_w4a8_gemm); C = int8 codes, q(v, s) =
+ * clamp(round_half_even(v / s), -128, 127) (fq_vit quantizer/uniform.py:23-45) */
+#define SAMQ_EPI_Q8 4          /* C i8 = q(y, out_scale)                  (Linear -> QAct)        */
+#define SAMQ_EPI_Q8_GELU 5     /* C i8 = q(GELU(y), out_scale)            (lin1 -> GELU -> QAct)  */
+#define SAMQ_EPI_Q8_RES 6      /* C i8 = q(R*res_scale + q(y,mid)*mid, out_scale)  (residual)   */
 
 /* Thread-local description of the last failure on this thread ("" if none). */
 const char* samq_last_error(void);
@@ -76,6 +81,49 @@ int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, cons
                         const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M,
                         int N, int K, int groupsize, int epilogue, int cfg, hipStream_t stream);
 
+/* ---------------------------------------------------------------- int8 activations */
+
+/* fq_vit int8 weights: W int8 [N][K] row-major (QLinear / flattened QConv2d weight codes,
+ * fq_vit/models/ptq/layers.py:160-200, 11-74) -> int8 MFMA fragment order (K*N bytes).
+ * K % 128 == 0, N % 32 == 0, 16-byte aligned pointers. */
+int samq_w8_repack(const int8_t* w, int8_t* packed, int K, int N, hipStream_t stream);
+
+/* W8A8 GEMM (fq_vit QLinear in quant mode, layers.py:190-200, fed by the int8 codes of the
+ * preceding QAct, layers.py:203-242):  y[m,n] = float(sum_k A[m,k] W[n,k]) * a_scale *
+ * wscale[n] + bias[n] (int32 exact sum), then the epilogue (SAMQ_EPI_*; Q8_RES reads the int8
+ * residual codes R (row stride ldr; may alias C) with res_scale and quantises y with mid_scale
+ * first when mid_scale > 0).  A int8 [M,K] (16-byte aligned, lda % 16 == 0); wpacked from
+ * samq_w8_repack; wscale/bias f32 [N] (bias may be NULL); K % 128 == 0, N % 64 == 0. */
+int samq_w8a8_gemm(const int8_t* A, int64_t lda, const int8_t* wpacked, const float* wscale,
+                   const float* bias, void* C, int64_t ldc, const int8_t* R, int64_t ldr, int M,
+                   int N, int K, int epilogue, float a_scale, float mid_scale, float res_scale,
+                   float out_scale, hipStream_t stream);
+
+/* W4A8 GEMM: GPTQ int4 weights (QuantLinear buffers, gptq_triton/quant_linear.py:81-85, repacked
+ * with samq_w4_repack_layout(..., layout 3, ...)) x int8 activation codes (fq_vit QAct on the
+ * QuantLinear input, SURVEY.md §8c "Oracle W4A8"): y = float(sum_k A (q - zp)) * a_scale *
+ * wscale[n] + bias[n]; wscale = the QuantLinear scales as f32 [N]; groupsize must be -1 (else
+ * SAMQ_ERR_UNSUPPORTED); epilogues BIAS/BIAS_GELU (f16 out), RESADD_F32/F32, Q8/Q8_GELU. */
+int samq_w4a8_gemm(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                   const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N,
+                   int K, int groupsize, int epilogue, float a_scale, float out_scale,
+                   hipStream_t stream);
+
+/* Both int8 GEMMs with an explicit weight format (0 = W8 packed, 1 = W4 layout 3) and tile
+ * config (0 = automatic; 81 256x256, 82 128x256, 83 128x128, 84 64x64); for tuning and tests. */
+int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked, const float* wscale,
+                     const int32_t* qzeros, const float* bias, void* C, int64_t ldc, const int8_t* R,
+                     int64_t ldr, int M, int N, int K, int epilogue, float a_scale, float mid_scale,
+                     float res_scale, float out_scale, int cfg, hipStream_t stream);
+
+/* Elementwise activation quantiser (fq_vit QAct in quant mode, layers.py:232-242 ->
+ * UniformQuantizer.forward, quantizer/base.py:43-49, uniform.py:23-45, zero point 0):
+ * codes[i] = q(x[i], scale); x f32 (or f16 with SAMQ_Q_IN_F16); with SAMQ_Q_OUT_FQ the output is
+ * the f32 fake-quant value codes*scale instead of int8 codes. */
+#define SAMQ_Q_IN_F16 1
+#define SAMQ_Q_OUT_FQ 2
+int samq_quantize(const void* x, void* y, int64_t n, float scale, int flags, hipStream_t stream);
+
 /* ---------------------------------------------------------------- normalisation */
 
 /* y[r,:] = LayerNorm(x[r,:]) * gamma + beta over C channels (row stride C), f32 statistics.
@@ -87,6 +135,18 @@ int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, cons
 #define SAMQ_LN_OUT_F32 2
 int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
                    int C, float eps, int flags, hipStream_t stream);
+
+/* LayerNorm with int8 activation codes on either side (fq_vit QIntLayerNorm = nn.LayerNorm
+ * between two QActs, layers.py:245-258, fq_vit/models/sam/image_encoder.py:310-331; neck
+ * QIntLayerNorm2D eps 1e-5, fq_vit/models/sam/common.py:93-108):
+ *   SAMQ_LN_IN_I8:  x = int8 codes * in_scale (else f32 / f16 per SAMQ_LN_IN_F16);
+ *   SAMQ_LN_OUT_I8: y = q(LN(x), out_scale) int8 codes; with SAMQ_LN_OUT_F32 as well, y is the
+ *   f32 fake-quant value q(..)*out_scale (else f16 / f32 per SAMQ_LN_OUT_F32). */
+#define SAMQ_LN_IN_I8 4
+#define SAMQ_LN_OUT_I8 8
+int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                     int C, float eps, int flags, float in_scale, float out_scale,
+                     hipStream_t stream);
 
 /* ---------------------------------------------------------------- attention */
 
@@ -117,6 +177,21 @@ int samq_rel_attention(const void* qkv, const void* qkv_bias, const void* rel_po
  * out f16 [B, S, S, heads*hd]. */
 int samq_attention_relbias(const void* inp, const void* rel_h, const void* rel_w, void* out, int B,
                            int S, int heads, int hd, float sm_scale, hipStream_t stream);
+
+/* W8A8 attention (fq_vit quant-mode Attention.forward, fq_vit/models/sam/image_encoder.py:437-478,
+ * with window_partition / window_unpartition :282-333 folded in) on int8 codes:
+ *   qkv  int8 [B, H, W, 3, heads, hd] codes of attn.qact1 (scale s_qkv), natural token order;
+ *   scores = q8((q*s_qkv*sm_scale).(k*s_qkv), s_a1) * s_a1            (qact_attn1)
+ *   scores = q8(scores + rel_h + rel_w, s_a2) * s_a2                   (use_rel_pos_qact; rel_w
+ *            indexed by the query ROW, quirk 1; rel tables f32 [2*side-1, hd])
+ *   out  int8 [B, H, W, heads*hd] = q8(softmax(scores) . (v*s_qkv), s_out)     (qact2)
+ * window > 0: S x S windows over the grid padded to a multiple of S (pad tokens' q/k/v =
+ * q8(qkv_bias f32 [3*heads*hd], s_qkv), or 0 if qkv_bias is NULL), window <= 16;
+ * window == 0: global over an H == W <= 64 grid.  hd must be 64 (else SAMQ_ERR_UNSUPPORTED). */
+int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
+                          const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads,
+                          int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
+                          float s_out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

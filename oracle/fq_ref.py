@@ -63,9 +63,12 @@ class FQEncoderOracle:
 
     WEIGHTS = ("patch_embed.proj", "neck.0", "neck.2")
 
-    def __init__(self, cfg: dict, state: dict):
+    def __init__(self, cfg: dict, state: dict, dtype: torch.dtype = torch.float32):
+        # dtype float64: the same fake-quant function evaluated with (nearly) exact arithmetic --
+        # used by the tests to measure how far fp32 rounding alone moves the reference's codes
         self.cfg = cfg
-        self.p = {k: _t(v, torch.float32) for k, v in state.items()}
+        self.dtype = dtype
+        self.p = {k: _t(v, dtype) for k, v in state.items()}
         self.minmax: dict[str, tuple[torch.Tensor, torch.Tensor]] = {}
         self.scales: dict[str, torch.Tensor] = {}
         self.mode = "float"  # "float" | "calib" | "quant"
@@ -75,8 +78,8 @@ class FQEncoderOracle:
         names = list(self.WEIGHTS) + [f"blocks.{i}.{s}" for i in range(cfg["depth"])
                                       for s in ("attn.qkv", "attn.proj", "mlp.lin1", "mlp.lin2")]
         for n in names:
-            wfq, s, _ = weight_fake_quant(self.p[n + ".weight"])
-            self.wq[n], self.wscale[n] = wfq, s
+            wfq, s, _ = weight_fake_quant(self.p[n + ".weight"].float())   # fp32 scales (the model's)
+            self.wq[n], self.wscale[n] = wfq.to(dtype), s
 
     # -- activation quantiser points ------------------------------------------------------
     def qact(self, name: str, x: torch.Tensor) -> torch.Tensor:
@@ -96,6 +99,11 @@ class FQEncoderOracle:
 
     def finalize(self):
         self.scales = {k: sym_scale(lo, hi) for k, (lo, hi) in self.minmax.items()}
+
+    def set_scales(self, scales: dict) -> None:
+        """Use calibrated activation scales (e.g. the reference's ``quantizer.scale`` buffers)."""
+        self.scales = {k: torch.tensor(float(v), dtype=torch.float32).to(self.dtype) for k, v in scales.items()}
+        self.mode = "quant"
 
     # -- graph -----------------------------------------------------------------------------
     def attention(self, pre: str, x: torch.Tensor) -> torch.Tensor:
@@ -144,7 +152,7 @@ class FQEncoderOracle:
     @torch.no_grad()
     def forward(self, img) -> torch.Tensor:
         p, cfg = self.p, self.cfg
-        x = self.qact("qact_input", _t(img, torch.float32))
+        x = self.qact("qact_input", _t(img, self.dtype))
         x = F.conv2d(x, self.w("patch_embed.proj"), p["patch_embed.proj.bias"], stride=cfg["patch_size"])
         x = self.qact("patch_embed.qact", x).permute(0, 2, 3, 1)
         x = x + self.qact("qact_pos", p["pos_embed"])

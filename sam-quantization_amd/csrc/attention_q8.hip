@@ -1,0 +1,316 @@
+// W8A8 (fq_vit) attention with decomposed relative position on int8 q/k/v codes, gfx950.
+//
+// Replaces fq_vit's quant-mode Attention.forward (fq_vit/models/sam/image_encoder.py:437-478):
+//   qkv   = qact1(qkv(x))                       -> int8 codes, per-tensor scale s_qkv (input)
+//   attn  = qact_attn1((q * scale) @ k^T)       -> quantised with s_a1
+//   attn  = use_rel_pos_qact(attn + rel_h + rel_w)   (add_decomposed_rel_pos, quirk-1 rel_w
+//           indexed by the query ROW, image_encoder.py:402)          -> quantised with s_a2
+//   attn  = softmax(attn)                       (QIntSoftmax = F.softmax, layers.py:379)
+//   o     = qact2(attn @ v)                     -> int8 codes with s_out (output, proj input)
+// together with window_partition / window_unpartition (padded tokens are keys/values whose qkv is
+// the fake-quantised qkv bias, exactly as the reference's zero-padded LayerNorm output projects).
+//
+// Arithmetic (all exact or fp32, SURVEY.md §8c Oracle F):
+//   * q.k on v_mfma_i32_16x16x64_i8: exact int32; value = int * (s_qkv * scale * s_qkv);
+//   * rel_h / rel_w: fp32 dot products of the fake-quant q (code * s_qkv) with the f32 tables;
+//   * the two score quantisers use a true division and round-half-to-even (uniform.py:31-36);
+//   * softmax in fp32 (online, exp of x - max as the reference), P.V on fp16 MFMA with P split
+//     hi + lo (both fp16; |P - hi - lo| ~ 2^-22 |P|) and the exact int8 V codes as fp16.
+// Layout: S^T = K.Q^T per 16-key block (lane = one query, 4 keys), so P^T feeds the P.V MFMA's B
+// operand from the same registers; V^T is staged in LDS as fp16 [d][key].
+//
+// Grid: (images * windows, heads, query tiles of 16*NWQ).  RESIDENT (windows, S*S <= 256 keys):
+// all keys staged once; otherwise 64-key chunks double-buffered through LDS.
+#include "common.h"
+
+namespace samq {
+
+struct AttnQ8Params {
+  const int8_t* qkv;        // [B, H, W, 3, heads, 64] codes
+  const float* qkv_bias;    // [3 * C] f32 or null (pad tokens)
+  const float* relh;        // [2S-1, 64] f32
+  const float* relw;        // [2S-1, 64] f32
+  int8_t* out;              // [B, H, W, C] codes
+  int B, H, W, heads, C, S, window, nwh, nww, L;
+  float qk_scale, s_qkv, s_a1, s_a2, s_out;
+};
+
+typedef int int4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float aq8(float v, float s) {
+  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);
+}
+
+constexpr int QD = 64;       // head dim (vit_b)
+constexpr int KPITCH = 80;   // K row pitch in LDS (bytes): conflict-free 16-byte fragment reads
+
+template <bool RESIDENT, int NWQ, int KC, int MAXS>
+__global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params p) {
+  constexpr int NBUF = RESIDENT ? 1 : 2;
+  constexpr int VTP = KC + 8;                    // V^T row pitch (halves)
+  __shared__ __attribute__((aligned(16))) int8_t k_lds[NBUF][KC * KPITCH];
+  __shared__ __attribute__((aligned(16))) _Float16 vt_lds[NBUF][QD * VTP];
+  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
+  __shared__ float rh_lds[NWQ][16 * (MAXS + 1)];
+  __shared__ float rw_lds[NWQ][16 * (MAXS + 1)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int ql = lane & 15;
+  const int S = p.S, L = p.L, C = p.C;
+  const int head = blockIdx.y;
+  int b, wy = 0, wx = 0;
+  if (p.window > 0) {
+    const int per = p.nwh * p.nww;
+    b = blockIdx.x / per;
+    wy = (blockIdx.x % per) / p.nww;
+    wx = blockIdx.x % p.nww;
+  } else {
+    b = blockIdx.x;
+  }
+  const float invS = 1.0f / (float)S;
+
+  // local token index -> (row, col) in the window / grid and validity in the image
+  auto tok = [&](int t, int& ty, int& tx) {
+    ty = (int)(((float)t + 0.5f) * invS);
+    tx = t - ty * S;
+  };
+  auto tok_ptr = [&](int ty, int tx, bool& inimg) -> const int8_t* {
+    const int y = wy * S + ty, x = wx * S + tx;
+    inimg = y < p.H && x < p.W;
+    return p.qkv + (((int64_t)b * p.H + y) * p.W + x) * (3 * C);
+  };
+
+  // ---- stage keys [c0, c0 + KC) of K (codes) and V^T (fp16) into buffer buf
+  auto stage = [&](int c0, int buf) {
+    for (int u = tid; u < KC * 4; u += 64 * NWQ) {
+      const int key = u % KC, part = u / KC;
+      const int kk = c0 + key;
+      u32x4 kc = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
+      if (kk < L) {
+        int ty, tx;
+        tok(kk, ty, tx);
+        bool inimg;
+        const int8_t* tp = tok_ptr(ty, tx, inimg);
+        if (inimg) {
+          kc = *(const u32x4*)(tp + C + head * QD + part * 16);
+          vc = *(const u32x4*)(tp + 2 * C + head * QD + part * 16);
+        } else if (p.qkv_bias) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int kq = (int)aq8(p.qkv_bias[C + head * QD + part * 16 + e], p.s_qkv);
+            const int vq = (int)aq8(p.qkv_bias[2 * C + head * QD + part * 16 + e], p.s_qkv);
+            kc[e >> 2] |= ((uint32_t)kq & 0xFFu) << (8 * (e & 3));
+            vc[e >> 2] |= ((uint32_t)vq & 0xFFu) << (8 * (e & 3));
+          }
+        }
+      }
+      *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kc;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        vt_lds[buf][(part * 16 + e) * VTP + key] = (_Float16)(float)(int8_t)((vc[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+    }
+  };
+
+  // ---- this wave's 16 queries: codes (B operand of S^T = K.Q^T) and the rel-pos terms
+  const int q0 = blockIdx.z * (16 * NWQ) + wave * 16;
+  const int qt = q0 + ql;
+  int qy = 0, qx = 0;
+  bool q_ok = false;
+  int4v qfrag = {0, 0, 0, 0};
+  if (qt < L) {
+    tok(qt, qy, qx);
+    bool inimg;
+    const int8_t* tp = tok_ptr(qy, qx, inimg);
+    q_ok = inimg;
+    if (inimg) {
+      qfrag = *(const int4v*)(tp + head * QD + g * 16);
+    } else if (p.qkv_bias) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qq = (int)aq8(p.qkv_bias[head * QD + g * 16 + e], p.s_qkv);
+        qfrag[e >> 2] |= (qq & 0xFF) << (8 * (e & 3));
+      }
+    }
+  }
+  *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  {
+    // rel_h[q][kh] = sum_d (code_q[d] * s_qkv) * Rh[qy - kh + S - 1][d];  rel_w likewise with Rw and
+    // the same ROW index qy (quirk 1).  16 lanes share one table row.
+    const int pairs = 16 * S;
+    for (int pi = lane; pi < pairs; pi += 64) {
+      const int qi = pi & 15, kk = pi >> 4;
+      const int qtt = q0 + qi;
+      int ty = 0, tx = 0;
+      if (qtt < L) tok(qtt, ty, tx);
+      const int ridx = ty - kk + S - 1;
+      const float* th = p.relh + (int64_t)ridx * QD;
+      const float* tw = p.relw + (int64_t)ridx * QD;
+      float ah = 0.f, aw = 0.f;
+#pragma unroll 1
+      for (int d4 = 0; d4 < QD / 16; ++d4) {
+        const u32x4 cw = *(const u32x4*)(&q_lds[wave][qi * KPITCH + d4 * 16]);
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
+          const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
+            ah = fmaf(qf, h4[e], ah);
+            aw = fmaf(qf, w4[e], aw);
+          }
+        }
+      }
+      rh_lds[wave][qi * (MAXS + 1) + kk] = ah;
+      rw_lds[wave][qi * (MAXS + 1) + kk] = aw;
+    }
+  }
+
+  const int nchunks = (L + 63) / 64;
+  float m = -INFINITY, lsum = 0.f;
+  float4_t acc[QD / 16];
+#pragma unroll
+  for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+  const float* rhq = &rh_lds[wave][ql * (MAXS + 1)];
+  const float* rwq = &rw_lds[wave][ql * (MAXS + 1)];
+
+  if (RESIDENT) {
+    for (int c0 = 0; c0 < L; c0 += KC) stage(c0, 0);   // KC >= L: one pass
+  } else {
+    stage(0, 0);
+  }
+  __syncthreads();
+
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int buf = RESIDENT ? 0 : (ch & 1);
+    const int koff = RESIDENT ? ch * 64 : 0;             // key offset inside the staged buffer
+    if (!RESIDENT && ch + 1 < nchunks) stage((ch + 1) * 64, buf ^ 1);
+    // ---- S^T block scores
+    float c2[4][4];
+    float cmax = -INFINITY;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int4v kf = *(const int4v*)(&k_lds[buf][(koff + bb * 16 + ql) * KPITCH + g * 16]);
+      const int4v z = {0, 0, 0, 0};
+      const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = ch * 64 + bb * 16 + 4 * g + i;
+        float c = -INFINITY;
+        if (key < L) {
+          int kh, kw;
+          tok(key, kh, kw);
+          const float v = (float)st[i] * p.qk_scale;
+          const float v1 = aq8(v, p.s_a1) * p.s_a1;
+          const float t = (v1 + rhq[kh]) + rwq[kw];
+          c = aq8(t, p.s_a2);
+        }
+        c2[bb][i] = c;
+        cmax = fmaxf(cmax, c);
+      }
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    if (cmax > m) {
+      const float alpha = m == -INFINITY ? 0.f : expf(m * p.s_a2 - cmax * p.s_a2);
+      lsum *= alpha;
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
+      m = cmax;
+    }
+    const float ms = m * p.s_a2;
+    float (&pr)[4][4] = c2;   // probabilities overwrite the score codes in place
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pv = c2[bb][i] == -INFINITY ? 0.f : expf(c2[bb][i] * p.s_a2 - ms);
+        pr[bb][i] = pv;
+        lsum += pv;
+      }
+    // ---- O^T += V^T . P^T  (two 32-key steps, P split hi + lo)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      half8_t bhi, blo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = pr[2 * s2 + (j >> 2)][j & 3];
+        const _Float16 h = (_Float16)pv;
+        bhi[j] = h;
+        blo[j] = (_Float16)(pv - (float)h);
+      }
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) {
+        const _Float16* vr = &vt_lds[buf][(t * 16 + ql) * VTP + koff + 32 * s2 + 4 * g];
+        const half4_t a0 = *(const half4_t*)vr;
+        const half4_t a1 = *(const half4_t*)(vr + 16);
+        const half8_t af = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bhi, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, blo, acc[t], 0, 0, 0);
+      }
+    }
+    if (!RESIDENT) __syncthreads();   // chunk ch+1 staged; everyone done reading buffer buf
+  }
+
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (q_ok) {
+    int8_t* op = p.out + (((int64_t)b * p.H + (wy * S + qy)) * p.W + (wx * S + qx)) * C + head * QD;
+#pragma unroll
+    for (int t = 0; t < QD / 16; ++t) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float o = acc[t][i] / lsum * p.s_qkv;
+        w |= ((uint32_t)(int)aq8(o, p.s_out) & 0xFFu) << (8 * i);
+      }
+      *(uint32_t*)(op + t * 16 + 4 * g) = w;
+    }
+  }
+}
+
+}  // namespace samq
+
+using namespace samq;
+
+extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
+                                     const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
+                                     int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
+                                     hipStream_t stream) {
+  SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention_q8: null pointer");
+  SAMQ_REQUIRE(hd == QD, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: head_dim must be 64");
+  SAMQ_REQUIRE(B > 0 && H > 0 && W > 0 && heads > 0, SAMQ_ERR_INVALID, "rel_attention_q8: bad shape");
+  SAMQ_REQUIRE(s_qkv > 0.f && s_a1 > 0.f && s_a2 > 0.f && s_out > 0.f, SAMQ_ERR_INVALID,
+               "rel_attention_q8: scales must be > 0");
+  SAMQ_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 3) == 0, SAMQ_ERR_INVALID,
+               "rel_attention_q8: qkv must be 16-byte aligned");
+  AttnQ8Params p{};
+  p.qkv = qkv; p.qkv_bias = qkv_bias; p.relh = rel_pos_h; p.relw = rel_pos_w; p.out = out;
+  p.B = B; p.H = H; p.W = W; p.heads = heads; p.C = heads * hd;
+  // (q * scale) . k with q = c_q * s_qkv, k = c_k * s_qkv  (fq_vit image_encoder.py:455)
+  p.qk_scale = (s_qkv * sm_scale) * s_qkv;
+  p.s_qkv = s_qkv; p.s_a1 = s_a1; p.s_a2 = s_a2; p.s_out = s_out;
+  if (window > 0) {
+    SAMQ_REQUIRE(window <= 16, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: window must be <= 16");
+    p.S = window; p.window = window;
+    p.nwh = (H + window - 1) / window; p.nww = (W + window - 1) / window;
+    p.L = window * window;
+    const dim3 grid(B * p.nwh * p.nww, heads, 1);
+    if (p.L <= 13 * 16)   // SAM's 14 x 14 windows: 13 waves of 16 queries
+      hipLaunchKernelGGL((rel_attention_q8_kernel<true, 13, 256, 16>), grid, dim3(64 * 13), 0, stream, p);
+    else
+      hipLaunchKernelGGL((rel_attention_q8_kernel<true, 16, 256, 16>), grid, dim3(64 * 16), 0, stream, p);
+  } else {
+    SAMQ_REQUIRE(H == W && H <= 64, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: global attention needs H == W <= 64");
+    p.S = H; p.window = 0; p.nwh = p.nww = 1; p.L = H * W;
+    constexpr int NWQ = 4;
+    const dim3 grid(B, heads, (p.L + 16 * NWQ - 1) / (16 * NWQ));
+    hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64>), grid, dim3(64 * NWQ), 0, stream, p);
+  }
+  SAMQ_LAUNCH_CHECK("rel_attention_q8 launch");
+  return SAMQ_OK;
+}

@@ -1,0 +1,435 @@
+// Int8-activation GEMMs on gfx950 int8 MFMA (v_mfma_i32_32x32x32_i8):
+//   W8A8: int8 per-output-channel symmetric weights x int8 per-tensor activations -- the fq_vit
+//         QLinear / QConv2d compute (fq_vit/models/ptq/layers.py:160-200, 11-74) whose inputs are
+//         the int8 codes of the preceding QAct (layers.py:203-242, quantizer/uniform.py:23-45);
+//   W4A8: GPTQ int4 weights (gptq_triton/quant_linear.py:66-116 buffers) x int8 activations --
+//         the composition "QuantLinear + fq_vit QAct on its input" (SURVEY.md §8c Oracle W4A8).
+//
+// C[m,n] = epilogue( float(sum_k a[m,k] * w[k,n]) * (a_scale * w_scale[n]) + bias[n] ), with the
+// integer sum EXACT in int32 (the reference sums the dequantised fp32 products; both agree up to
+// fp32 rounding of the final value).  W4: w = q - zp, converted to int8 in registers:
+//   bytes(q) | 0x80 minus zp per byte never borrows (q in [0,15], zp in [1,16]), ^0x80 -> int8.
+//
+// Same machinery as the W4A16 v3 kernel (gemm_w4a16.hip): 3-slot LDS ring fed by
+// global_load_lds (A rows XOR-swizzled through the source address, B pre-packed in fragment
+// order), counted vmcnt waits + one s_barrier per K tile, XCD-aware tile remap, LDS-staged
+// 16-byte vector epilogue.  K tile = 128 int8 = the same 128-byte A rows as the fp16 kernel.
+//
+// Quantising epilogues (int8 output codes, fq_vit fake quant with a TRUE division and
+// round-half-to-even, clamp [-128, 127]):
+//   Q8      out = q(y, out_scale)                                  (Linear -> QAct)
+//   Q8_GELU out = q(GELU(y), out_scale)                            (lin1 -> GELU -> mlp.qact1)
+//   Q8_RES  out = q(R * res_scale + fq(y, mid_scale), out_scale)   (proj -> qact3 -> +x -> qact2)
+//           (mid_scale <= 0: no intermediate quantiser); R int8 codes, may alias C.
+#include "common.h"
+
+namespace samq {
+
+enum { BF_W8 = 0, BF_W4 = 1 };
+
+struct I8Epi {
+  float a_scale, mid_scale, res_scale, out_scale;
+  const int8_t* R;
+  int64_t ldr;
+};
+
+__device__ __forceinline__ float q8f(float v, float s) {
+  // clamp(round_half_even(v / s), -128, 127)   (quantizer/uniform.py:31-36, true division)
+  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait_i8() {
+  static_assert(N >= 0 && N <= 15, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int w4_to_i8(uint32_t nib, uint32_t zpx) {
+  return (int)(((nib | 0x80808080u) - zpx) ^ 0x80808080u);
+}
+
+// ------------------------------------------------------------------ W8 repack
+// packed byte (((nt * (K/128) + kb) * 4 + s) * 64 + lane) * 16 + j  =  W[n][k] with
+// n = nt*32 + (lane&31), k = kb*128 + 32*s + 16*(lane>>5) + j   (W row-major [N][K], i.e. the
+// nn.Linear / flattened Conv2d weight layout).
+__global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restrict__ out, int K, int N) {
+  const int64_t units = (int64_t)K * N / 16;
+  for (int64_t u = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = u & 63;
+    const int s = (u >> 6) & 3;
+    const int64_t blk = u >> 8;
+    const int kbs = K / 128;
+    const int kb = (int)(blk % kbs), nt = (int)(blk / kbs);
+    const int n = nt * 32 + (lane & 31);
+    const int k = kb * 128 + 32 * s + 16 * (lane >> 5);
+    *(u32x4*)(out + u * 16) = *(const u32x4*)(w + (int64_t)n * K + k);
+  }
+}
+
+// ------------------------------------------------------------------ GEMM
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
+void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
+                    const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
+                    const float* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
+                    int M, int N, int K, I8Epi ep_args) {
+  constexpr int NW = WAVES_M * WAVES_N;
+  constexpr int WM = BM / WAVES_M;
+  constexpr int WN = BN / WAVES_N;
+  constexpr int TM = WM / 32;
+  constexpr int TN = WN / 32;
+  constexpr int BK = 128;                     // int8 k per tile = 128-byte A rows
+  constexpr int ROWB = BK;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int PPB = BFMT == BF_W8 ? 4 : 2;  // 1-KiB pieces per (32-column, 128-k) block
+  constexpr int NA = BM / 8;
+  constexpr int NB = (BN / 32) * PPB;
+  constexpr int NT = NA + NB;
+  constexpr int NPW = (NT + NW - 1) / NW;
+  constexpr int STAGE = A_BYTES + NB * 1024;
+  static_assert(TM >= 1 && TN >= 1 && NPW <= 15, "bad tile");
+
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = K / BK;
+
+  const char* src[NPW];
+  int dst[NPW];
+  int64_t step[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    int j = wave * NPW + i;
+    j = j < NT ? j : NT - 1;
+    if (j < NA) {
+      const int row = j * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      src[i] = (const char*)(A + (int64_t)gr * lda + c * 16);
+      dst[i] = j * 1024;
+      step[i] = BK;
+    } else {
+      const int jb = j - NA;
+      const int nt = n0 / 32 + jb / PPB;
+      src[i] = Wp + (((int64_t)nt * kt_count) * PPB + (jb % PPB)) * 1024 + lane * 16;
+      dst[i] = A_BYTES + jb * 1024;
+      step[i] = PPB * 1024;
+    }
+  }
+  auto issue = [&](int kt, int slot) {
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + kt * step[i]),
+                                       (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+  };
+
+  int col[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+  uint32_t zpx[TN];
+  if (BFMT == BF_W4) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      const uint32_t zw = qzeros[col[t] >> 3];
+      zpx[t] = (((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u) * 0x01010101u;
+    }
+  }
+
+  int16_t_v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  int a_off[TM], a_swz[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_off[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
+  }
+  const int hsel = lane >> 5;
+  uint32_t kLo = 0x0F0F0F0Fu;
+  asm volatile("" : "+v"(kLo));
+
+  issue(0, 0);
+  if (STAGES > 2 && kt_count > 1) issue(1, 1);
+  int slot = 0;
+  for (int kt = 0; kt < kt_count; ++kt) {
+    if (STAGES > 2) {
+      if (kt + 1 < kt_count) vm_wait_i8<NPW>(); else vm_wait_i8<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < kt_count) {
+        int s2 = slot + 2;
+        s2 = s2 >= STAGES ? s2 - STAGES : s2;
+        issue(kt + 2, s2);
+      }
+    } else {
+      vm_wait_i8<0>();
+      __builtin_amdgcn_s_barrier();            // tile kt landed; everyone is done with tile kt-1
+      if (kt + 1 < kt_count) issue(kt + 1, slot ^ 1);
+    }
+    const char* abase = smem + slot * STAGE;
+    const char* bbase = abase + A_BYTES + (wn * TN) * PPB * 1024 + lane * 16;
+    u32x4 bw[TN][2];
+    if (BFMT == BF_W4) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        bw[t][0] = *(const u32x4*)(bbase + (t * PPB + 0) * 1024);
+        bw[t][1] = *(const u32x4*)(bbase + (t * PPB + 1) * 1024);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      int4_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const int4_t*)(abase + a_off[i] + (((2 * s + hsel) ^ a_swz[i]) << 4));
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        int4_t bf;
+        if (BFMT == BF_W8) {
+          bf = *(const int4_t*)(bbase + (t * PPB + s) * 1024);
+        } else {
+          const uint32_t w0 = bw[t][s >> 1][2 * (s & 1)];
+          const uint32_t w1 = bw[t][s >> 1][2 * (s & 1) + 1];
+          bf[0] = w4_to_i8(w0 & kLo, zpx[t]);
+          bf[1] = w4_to_i8((w0 >> 4) & kLo, zpx[t]);
+          bf[2] = w4_to_i8(w1 & kLo, zpx[t]);
+          bf[3] = w4_to_i8((w1 >> 4) & kLo, zpx[t]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf, acc[i][t], 0, 0, 0);
+      }
+    }
+    if (STAGES > 2) slot = slot + 1 == STAGES ? 0 : slot + 1;
+    else slot ^= 1;
+  }
+
+  // ---- epilogue (LDS-staged per 32-row slice; see gemm_w4a16.hip v3)
+  float csc[TN], cb[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    csc[t] = ep_args.a_scale * wscale[col[t]];
+    cb[t] = bias ? bias[col[t]] : 0.0f;
+  }
+  constexpr int EP_BYTES = 32 * WN * 4;
+  static_assert(NW * EP_BYTES <= STAGES * STAGE, "epilogue staging does not fit the LDS ring");
+  __syncthreads();
+  float* ep = (float*)(smem + wave * EP_BYTES);
+  const int row_base = m0 + wm * WM;
+  const int col_base = n0 + wn * WN;
+  constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        float v = (float)acc[i][t][r] * csc[t] + cb[t];
+        if (GELU) v = gelu_fast(v);
+        ep[rl * WN + t * 32 + (lane & 31)] = v;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+      constexpr int C4 = WN / 4;
+#pragma unroll
+      for (int j = 0; j < 32 * C4 / 64; ++j) {
+        const int idx = j * 64 + lane;
+        const int rl = idx / C4, c4 = idx % C4;
+        const int row = row_base + i * 32 + rl;
+        const float4_t v = ((const float4_t*)ep)[idx];
+        if (row < M) {
+          float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
+          if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+        }
+      }
+    } else if (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) {
+      constexpr int C8 = WN / 8;
+#pragma unroll
+      for (int j = 0; j < (32 * C8 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < 32 * C8) {
+          const int rl = idx / C8, c8 = idx % C8;
+          const int row = row_base + i * 32 + rl;
+          const float4_t v0 = ((const float4_t*)ep)[2 * idx];
+          const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+          if (row < M) {
+            const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                               (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+            *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
+          }
+        }
+      }
+    } else {   // int8 codes, 16 columns per lane-store
+      constexpr int C16 = WN / 16;
+#pragma unroll
+      for (int j = 0; j < (32 * C16 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < 32 * C16) {
+          const int rl = idx / C16, c16 = idx % C16;
+          const int row = row_base + i * 32 + rl;
+          if (row < M) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float4_t f = ((const float4_t*)ep)[4 * idx + e];
+              v[4 * e] = f[0]; v[4 * e + 1] = f[1]; v[4 * e + 2] = f[2]; v[4 * e + 3] = f[3];
+            }
+            u32x4 res;
+            if (EPI == SAMQ_EPI_Q8_RES)
+              res = *(const u32x4*)(ep_args.R + (int64_t)row * ep_args.ldr + col_base + 16 * c16);
+            u32x4 o;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              uint32_t word = 0;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                float x = v[4 * w + b];
+                if (EPI == SAMQ_EPI_Q8_RES) {
+                  if (ep_args.mid_scale > 0.f) x = q8f(x, ep_args.mid_scale) * ep_args.mid_scale;
+                  const float rv = (float)(int8_t)((res[w] >> (8 * b)) & 0xFFu) * ep_args.res_scale;
+                  x = rv + x;
+                }
+                const int qv = (int)q8f(x, ep_args.out_scale);
+                word |= ((uint32_t)qv & 0xFFu) << (8 * b);
+              }
+              o[w] = word;
+            }
+            *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
+
+struct I8Args {
+  const int8_t* A; int64_t lda; const char* Wp; const float* wscale; const uint32_t* qzeros;
+  const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep;
+};
+
+template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST>
+static int launch_i8(const I8Args& a, hipStream_t st) {
+  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+                     a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep);
+  SAMQ_LAUNCH_CHECK("i8_gemm launch");
+  return SAMQ_OK;
+}
+
+// tile configs: 81 256x256 (W4: 3 stages; W8: 2), 82 128x256, 83 128x128, 84 64x64
+template <int EPI, int BF>
+static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 81:
+      if constexpr (BF == BF_W4) return launch_i8<256, 256, 2, 4, EPI, BF, 3>(a, st);
+      else return launch_i8<256, 256, 2, 4, EPI, BF, 2>(a, st);
+    case 82: return launch_i8<128, 256, 2, 4, EPI, BF, 3>(a, st);
+    case 83: return launch_i8<128, 128, 2, 2, EPI, BF, 3>(a, st);
+    case 84: return launch_i8<64, 64, 2, 2, EPI, BF, 3>(a, st);
+    default: return fail(SAMQ_ERR_INVALID, "i8_gemm: unknown tile config");
+  }
+}
+
+static int i8_cfg_bn(int cfg) {
+  switch (cfg) { case 81: case 82: return 256; case 83: return 128; case 84: return 64; default: return 0; }
+}
+
+static int i8_pick_cfg(int M, int N) {
+  const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);
+  if (N % 256 == 0 && t256 >= 512) return 82;
+  if (N % 128 == 0 && M >= 256) return 83;
+  return 84;
+}
+
+static int i8_dispatch(const I8Args& a, int bfmt, int epi, int cfg, hipStream_t st) {
+#define I8_EPI(E) \
+  case E: return bfmt == BF_W8 ? launch_i8_cfg<E, BF_W8>(a, cfg, st) : launch_i8_cfg<E, BF_W4>(a, cfg, st)
+  switch (epi) {
+    I8_EPI(SAMQ_EPI_BIAS);
+    I8_EPI(SAMQ_EPI_BIAS_GELU);
+    I8_EPI(SAMQ_EPI_RESADD_F32);
+    I8_EPI(SAMQ_EPI_F32);
+    I8_EPI(SAMQ_EPI_Q8);
+    I8_EPI(SAMQ_EPI_Q8_GELU);
+    I8_EPI(SAMQ_EPI_Q8_RES);
+    default: return fail(SAMQ_ERR_INVALID, "i8_gemm: unknown epilogue");
+  }
+#undef I8_EPI
+}
+
+}  // namespace samq
+
+using namespace samq;
+
+extern "C" int samq_w8_repack(const int8_t* w, int8_t* packed, int K, int N, hipStream_t stream) {
+  SAMQ_REQUIRE(w && packed, SAMQ_ERR_INVALID, "w8_repack: null pointer");
+  SAMQ_REQUIRE(K > 0 && K % 128 == 0, SAMQ_ERR_INVALID, "w8_repack: K must be a positive multiple of 128");
+  SAMQ_REQUIRE(N > 0 && N % 32 == 0, SAMQ_ERR_INVALID, "w8_repack: N must be a multiple of 32");
+  SAMQ_REQUIRE(((uintptr_t)w & 15) == 0 && ((uintptr_t)packed & 15) == 0, SAMQ_ERR_INVALID,
+               "w8_repack: pointers must be 16-byte aligned");
+  const int64_t units = (int64_t)K * N / 16;
+  const int blocks = (int)((units + 255) / 256 < 8192 ? (units + 255) / 256 : 8192);
+  hipLaunchKernelGGL(w8_repack_kernel, dim3(blocks), dim3(256), 0, stream, w, packed, K, N);
+  SAMQ_LAUNCH_CHECK("w8_repack launch");
+  return SAMQ_OK;
+}
+
+extern "C" int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked, const float* wscale,
+                                const int32_t* qzeros, const float* bias, void* C, int64_t ldc, const int8_t* R,
+                                int64_t ldr, int M, int N, int K, int epilogue, float a_scale, float mid_scale,
+                                float res_scale, float out_scale, int cfg, hipStream_t stream) {
+  SAMQ_REQUIRE(A && wpacked && wscale && C, SAMQ_ERR_INVALID, "i8_gemm: null pointer");
+  SAMQ_REQUIRE(bfmt == BF_W8 || bfmt == BF_W4, SAMQ_ERR_INVALID, "i8_gemm: unknown weight format");
+  SAMQ_REQUIRE(bfmt == BF_W8 || qzeros, SAMQ_ERR_INVALID, "i8_gemm: W4 needs qzeros");
+  SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 128 == 0, SAMQ_ERR_INVALID, "i8_gemm: K must be a multiple of 128");
+  SAMQ_REQUIRE(N % 64 == 0, SAMQ_ERR_INVALID, "i8_gemm: N must be a multiple of 64");
+  SAMQ_REQUIRE(lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0, SAMQ_ERR_INVALID,
+               "i8_gemm: A must be 16-byte aligned with lda >= K, lda % 16 == 0");
+  SAMQ_REQUIRE(ldc >= N && ((uintptr_t)C & 15) == 0, SAMQ_ERR_INVALID, "i8_gemm: C must be 16-byte aligned, ldc >= N");
+  const bool q8 = epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_GELU || epilogue == SAMQ_EPI_Q8_RES;
+  const bool f32 = epilogue == SAMQ_EPI_RESADD_F32 || epilogue == SAMQ_EPI_F32;
+  SAMQ_REQUIRE(ldc % (q8 ? 16 : (f32 ? 4 : 8)) == 0, SAMQ_ERR_INVALID, "i8_gemm: ldc breaks 16-byte row alignment");
+  SAMQ_REQUIRE(!q8 || out_scale > 0.f, SAMQ_ERR_INVALID, "i8_gemm: quantising epilogue needs out_scale > 0");
+  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES || (R && ldr % 16 == 0 && ((uintptr_t)R & 15) == 0), SAMQ_ERR_INVALID,
+               "i8_gemm: Q8_RES needs a 16-byte aligned residual R with ldr % 16 == 0");
+  if (M == 0) return SAMQ_OK;
+  if (cfg <= 0) cfg = i8_pick_cfg(M, N);
+  SAMQ_REQUIRE(i8_cfg_bn(cfg) > 0 && N % i8_cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "i8_gemm: N not divisible by tile");
+  I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
+           I8Epi{a_scale, mid_scale, res_scale, out_scale, R, ldr}};
+  return i8_dispatch(a, bfmt, epilogue, cfg, stream);
+}
+
+extern "C" int samq_w8a8_gemm(const int8_t* A, int64_t lda, const int8_t* wpacked, const float* wscale,
+                              const float* bias, void* C, int64_t ldc, const int8_t* R, int64_t ldr, int M, int N,
+                              int K, int epilogue, float a_scale, float mid_scale, float res_scale, float out_scale,
+                              hipStream_t stream) {
+  return samq_i8_gemm_cfg(A, lda, BF_W8, wpacked, wscale, nullptr, bias, C, ldc, R, ldr, M, N, K, epilogue, a_scale,
+                          mid_scale, res_scale, out_scale, 0, stream);
+}
+
+extern "C" int samq_w4a8_gemm(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                              const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N, int K,
+                              int groupsize, int epilogue, float a_scale, float out_scale, hipStream_t stream) {
+  SAMQ_REQUIRE(groupsize == -1 || groupsize == K, SAMQ_ERR_UNSUPPORTED,
+               "w4a8_gemm: only per-channel weights (groupsize -1) are supported with int8 activations");
+  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES, SAMQ_ERR_INVALID, "w4a8_gemm: Q8_RES is a W8A8 epilogue");
+  return samq_i8_gemm_cfg(A, lda, BF_W4, wpacked, wscale, qzeros, bias, C, ldc, nullptr, 0, M, N, K, epilogue,
+                          a_scale, 0.f, 0.f, out_scale, 0, stream);
+}

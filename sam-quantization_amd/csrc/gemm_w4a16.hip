@@ -39,6 +39,11 @@ namespace samq {
 // k = kb*64 + 16*s + 8*(lane>>5) + {0..7}, nibble order [k0,k2,k4,k6 | k1,k3,k5,k7].
 // LAYOUT 2 (v_mfma_f32_16x16x32_f16 fragments): word w of lane l in block (nt, kb) holds column
 // nt*32 + 16*(w>>1) + (l&15), k = kb*64 + 32*(w&1) + 8*(l>>4) + {0..7}; same nibble interleave.
+// LAYOUT 3 (int8 MFMA fragments of v_mfma_i32_32x32x32_i8, used by the W4A8 GEMM in gemm_i8.hip):
+// 2-KiB blocks (nt, kb) over 128-deep K tiles, two 1-KiB pieces p; word w of lane l in piece p
+// holds column nt*32 + (l&31), k = kb*128 + 32*(2p + (w>>1)) + 16*(l>>5) + 8*(w&1) + {0..7} with
+// nibble order [k0,k4,k1,k5,k2,k6,k3,k7], so (w & 0x0F0F0F0F) are the bytes k0..k3 and
+// ((w >> 4) & 0x0F0F0F0F) the bytes k4..k7.
 template <int LAYOUT>
 __global__ void w4_repack_kernel(const uint32_t* __restrict__ qweight, uint32_t* __restrict__ out,
                                  int K, int N) {
@@ -47,6 +52,24 @@ __global__ void w4_repack_kernel(const uint32_t* __restrict__ qweight, uint32_t*
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int s = idx & 3;
     const int lane = (idx >> 2) & 63;
+    if (LAYOUT == 3) {
+      const int p = (idx >> 8) & 1;
+      const int64_t blk = idx >> 9;            // nt * (K/128) + kb
+      const int kbs = K / 128;
+      const int kb = (int)(blk % kbs);
+      const int nt = (int)(blk / kbs);
+      const int n = nt * 32 + (lane & 31);
+      const int k0 = kb * 128 + 32 * (2 * p + (s >> 1)) + 16 * (lane >> 5) + 8 * (s & 1);
+      const uint32_t w = qweight[(int64_t)(k0 >> 3) * N + n];
+      uint32_t o = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o |= ((w >> (4 * i)) & 0xFu) << (8 * i);            // q[i]   -> byte i, low nibble
+        o |= ((w >> (4 * i + 16)) & 0xFu) << (8 * i + 4);   // q[i+4] -> byte i, high nibble
+      }
+      out[idx] = o;
+      continue;
+    }
     const int64_t blk = idx >> 8;             // nt * (K/64) + kb
     const int kbs = K / 64;
     const int kb = (int)(blk % kbs);
@@ -772,10 +795,14 @@ extern "C" int samq_w4_repack_layout(const int32_t* qweight, int32_t* packed, in
   SAMQ_REQUIRE(qweight && packed, SAMQ_ERR_INVALID, "w4_repack: null pointer");
   SAMQ_REQUIRE(K > 0 && N > 0 && K % 64 == 0, SAMQ_ERR_INVALID, "w4_repack: K must be a positive multiple of 64");
   SAMQ_REQUIRE(N % 32 == 0, SAMQ_ERR_INVALID, "w4_repack: N must be a multiple of 32");
-  SAMQ_REQUIRE(layout == 1 || layout == 2, SAMQ_ERR_INVALID, "w4_repack: layout must be 1 or 2");
+  SAMQ_REQUIRE(layout >= 1 && layout <= 3, SAMQ_ERR_INVALID, "w4_repack: layout must be 1, 2 or 3");
+  SAMQ_REQUIRE(layout != 3 || K % 128 == 0, SAMQ_ERR_INVALID, "w4_repack: layout 3 needs K % 128 == 0");
   const int64_t total = (int64_t)K * N / 8;
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  if (layout == 2)
+  if (layout == 3)
+    hipLaunchKernelGGL(w4_repack_kernel<3>, dim3(blocks), dim3(256), 0, stream, (const uint32_t*)qweight,
+                       (uint32_t*)packed, K, N);
+  else if (layout == 2)
     hipLaunchKernelGGL(w4_repack_kernel<2>, dim3(blocks), dim3(256), 0, stream, (const uint32_t*)qweight,
                        (uint32_t*)packed, K, N);
   else

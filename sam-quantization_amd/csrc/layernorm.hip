@@ -6,11 +6,19 @@
 
 namespace samq {
 
-template <bool IN_F16, bool OUT_F32, int VPT>  // VPT = float4 (or half4) vectors per lane
+// IN: 0 f32, 1 f16, 2 int8 codes (x = code * in_scale)
+// OUT: 0 f16, 1 f32, 2 int8 codes q(y, out_scale), 3 f32 fake-quant q(y, out_scale) * out_scale
+enum { LN_F32 = 0, LN_F16 = 1, LN_I8 = 2, LN_FQ32 = 3 };
+
+__device__ __forceinline__ float ln_q8(float v, float s) {
+  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);   // fq_vit uniform.py:31-36
+}
+
+template <int IN, int OUT, int VPT>  // VPT = 4-channel vectors per lane
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ xin, void* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows, int C,
-                                                        float eps) {
+                                                        float eps, float in_scale, float out_scale) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -21,9 +29,13 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
   for (int i = 0; i < VPT; ++i) {
     const int j = lane + 64 * i;
     if (j < nvec) {
-      if (IN_F16) {
+      if (IN == LN_F16) {
         const half4_t h = ((const half4_t*)xin)[row * nvec + j];
         v[i] = float4_t{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+      } else if (IN == LN_I8) {
+        const uint32_t w = ((const uint32_t*)xin)[row * nvec + j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[i][e] = (float)(int8_t)((w >> (8 * e)) & 0xFFu) * in_scale;
       } else {
         v[i] = ((const float4_t*)xin)[row * nvec + j];
       }
@@ -55,8 +67,17 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
       float4_t o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
-      if (OUT_F32) {
+      if (OUT == LN_F32) {
         ((float4_t*)y)[row * nvec + j] = o;
+      } else if (OUT == LN_FQ32) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = ln_q8(o[e], out_scale) * out_scale;
+        ((float4_t*)y)[row * nvec + j] = o;
+      } else if (OUT == LN_I8) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)ln_q8(o[e], out_scale) & 0xFFu) << (8 * e);
+        ((uint32_t*)y)[row * nvec + j] = w;
       } else {
         ((half4_t*)y)[row * nvec + j] = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
       }
@@ -68,25 +89,45 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 
 using namespace samq;
 
-extern "C" int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
-                              float eps, int flags, hipStream_t stream) {
+static int ln_launch(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C, float eps,
+                     int in, int out, float in_scale, float out_scale, hipStream_t stream) {
   SAMQ_REQUIRE(x && y && gamma && beta, SAMQ_ERR_INVALID, "layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 4096, SAMQ_ERR_INVALID, "layernorm: C must be a multiple of 4, <= 4096");
   if (rows <= 0) return SAMQ_OK;
   const dim3 grid((unsigned)((rows + 3) / 4));
   const int vpt = (C / 4 + 63) / 64;
-  const bool in16 = flags & SAMQ_LN_IN_F16, out32 = flags & SAMQ_LN_OUT_F32;
 #define LN_V(I, O) \
   do { \
-    if (vpt <= 1) hipLaunchKernelGGL((layernorm_kernel<I, O, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps); \
-    else if (vpt <= 3) hipLaunchKernelGGL((layernorm_kernel<I, O, 3>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps); \
-    else if (vpt <= 4) hipLaunchKernelGGL((layernorm_kernel<I, O, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps); \
-    else if (vpt <= 5) hipLaunchKernelGGL((layernorm_kernel<I, O, 5>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps); \
-    else hipLaunchKernelGGL((layernorm_kernel<I, O, 16>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps); \
+    if (vpt <= 1) hipLaunchKernelGGL((layernorm_kernel<I, O, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else if (vpt <= 3) hipLaunchKernelGGL((layernorm_kernel<I, O, 3>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else if (vpt <= 4) hipLaunchKernelGGL((layernorm_kernel<I, O, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else if (vpt <= 5) hipLaunchKernelGGL((layernorm_kernel<I, O, 5>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else hipLaunchKernelGGL((layernorm_kernel<I, O, 16>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
   } while (0)
-  if (in16) { if (out32) LN_V(true, true); else LN_V(true, false); }
-  else { if (out32) LN_V(false, true); else LN_V(false, false); }
+#define LN_O(I) \
+  do { \
+    switch (out) { case LN_F16: LN_V(I, LN_F16); break; case LN_F32: LN_V(I, LN_F32); break; \
+                   case LN_I8: LN_V(I, LN_I8); break; default: LN_V(I, LN_FQ32); break; } \
+  } while (0)
+  switch (in) { case LN_F16: LN_O(LN_F16); break; case LN_I8: LN_O(LN_I8); break; default: LN_O(LN_F32); break; }
+#undef LN_O
 #undef LN_V
   SAMQ_LAUNCH_CHECK("layernorm launch");
   return SAMQ_OK;
+}
+
+extern "C" int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
+                              float eps, int flags, hipStream_t stream) {
+  return ln_launch(x, y, gamma, beta, rows, C, eps, (flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32,
+                   (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, stream);
+}
+
+extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
+                                float eps, int flags, float in_scale, float out_scale, hipStream_t stream) {
+  SAMQ_REQUIRE(!(flags & SAMQ_LN_IN_I8) || in_scale > 0.f, SAMQ_ERR_INVALID, "layernorm_q: in_scale must be > 0");
+  SAMQ_REQUIRE(!(flags & SAMQ_LN_OUT_I8) || out_scale > 0.f, SAMQ_ERR_INVALID, "layernorm_q: out_scale must be > 0");
+  const int in = (flags & SAMQ_LN_IN_I8) ? LN_I8 : ((flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32);
+  const int out = (flags & SAMQ_LN_OUT_I8) ? ((flags & SAMQ_LN_OUT_F32) ? LN_FQ32 : LN_I8)
+                                           : ((flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16);
+  return ln_launch(x, y, gamma, beta, rows, C, eps, in, out, in_scale, out_scale, stream);
 }

@@ -21,9 +21,20 @@ EPI_BIAS = 0
 EPI_BIAS_GELU = 1
 EPI_RESADD_F32 = 2
 EPI_F32 = 3
+EPI_Q8 = 4
+EPI_Q8_GELU = 5
+EPI_Q8_RES = 6
+
+BF_W8 = 0
+BF_W4 = 1
+
+Q_IN_F16 = 1
+Q_OUT_FQ = 2
 
 LN_IN_F16 = 1
 LN_OUT_F32 = 2
+LN_IN_I8 = 4
+LN_OUT_I8 = 8
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -39,9 +50,20 @@ SIGNATURES = {
     "samq_w4_repack_layout": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "samq_w8_repack": (_i32, [_vp, _vp, _i32, _i32, _vp]),
+    "samq_w8a8_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32,
+                              _f32, _f32, _f32, _f32, _vp]),
+    "samq_w4a8_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
+                              _f32, _f32, _vp]),
+    "samq_i8_gemm_cfg": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
+                                _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
+    "samq_quantize": (_i32, [_vp, _vp, _i64, _f32, _i32, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
+    "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),
     "samq_rel_attention": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp]),
     "samq_attention_relbias": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _f32, _vp]),
+    "samq_rel_attention_q8": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _f32,
+                                     _f32, _f32, _f32, _vp]),
 }
 
 

@@ -15,6 +15,10 @@ EPI_BIAS = _lib.EPI_BIAS
 EPI_BIAS_GELU = _lib.EPI_BIAS_GELU
 EPI_RESADD_F32 = _lib.EPI_RESADD_F32
 EPI_F32 = _lib.EPI_F32
+EPI_Q8 = _lib.EPI_Q8
+EPI_Q8_GELU = _lib.EPI_Q8_GELU
+EPI_Q8_RES = _lib.EPI_Q8_RES
+_Q8_EPIS = (EPI_Q8, EPI_Q8_GELU, EPI_Q8_RES)
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -121,4 +125,122 @@ def attention_relbias(inp: torch.Tensor, rel_h: torch.Tensor, rel_w: torch.Tenso
     _lib.check(_lib.load().samq_attention_relbias(_ptr(inp.contiguous()), _ptr(rel_h.half().contiguous()),
                                                   _ptr(rel_w.half().contiguous()), _ptr(out), b, h, heads, hd,
                                                   float(sm_scale), _stream()), "attention_relbias")
+    return out
+
+
+# ----------------------------------------------------------------------------- int8 activations
+def quantize(x: torch.Tensor, scale: float, fake: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fq_vit QAct (quant mode): int8 codes ``clamp(round(x / s), -128, 127)`` (or, with
+    ``fake``, the f32 value ``codes * s``).  x f32 / f16 contiguous."""
+    _need_cuda(x)
+    assert x.is_contiguous() and x.dtype in (torch.float32, torch.float16)
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.float32 if fake else torch.int8, device=x.device)
+    flags = (_lib.Q_IN_F16 if x.dtype == torch.float16 else 0) | (_lib.Q_OUT_FQ if fake else 0)
+    _lib.check(_lib.load().samq_quantize(_ptr(x), _ptr(out), x.numel(), float(scale), flags, _stream()), "quantize")
+    return out
+
+
+def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, in_scale: float = 0.0,
+                out_scale: float = 0.0, out_dtype: torch.dtype = torch.int8,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """LayerNorm with int8 codes on either side: x int8 (codes * in_scale) / f32 / f16;
+    out int8 codes (q(y, out_scale)), f32 fake-quant (out_dtype f32 with out_scale > 0), f16 or f32."""
+    _need_cuda(x, gamma, beta)
+    c = x.shape[-1]
+    assert x.is_contiguous() and gamma.dtype == torch.float32 and beta.dtype == torch.float32
+    if out is None:
+        out = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+    flags = 0
+    if x.dtype == torch.int8:
+        flags |= _lib.LN_IN_I8
+    elif x.dtype == torch.float16:
+        flags |= _lib.LN_IN_F16
+    if out.dtype == torch.int8:
+        flags |= _lib.LN_OUT_I8
+    elif out.dtype == torch.float32:
+        flags |= _lib.LN_OUT_F32 | (_lib.LN_OUT_I8 if out_scale > 0 else 0)
+    _lib.check(_lib.load().samq_layernorm_q(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), x.numel() // c, c,
+                                            float(eps), flags, float(in_scale), float(out_scale), _stream()),
+               "layernorm_q")
+    return out
+
+
+def w8_repack(w: torch.Tensor) -> torch.Tensor:
+    """int8 weight codes [N, K] (QLinear / flattened QConv2d layout) -> int8 MFMA fragment order."""
+    _need_cuda(w)
+    assert w.dtype == torch.int8 and w.dim() == 2
+    w = w.contiguous()
+    n, k = w.shape
+    out = torch.empty(n * k, dtype=torch.int8, device=w.device)
+    _lib.check(_lib.load().samq_w8_repack(_ptr(w), _ptr(out), k, n, _stream()), "w8_repack")
+    return out
+
+
+def _i8_out(a2, n, epilogue, out, shape):
+    if out is None:
+        if epilogue in _Q8_EPIS:
+            dt = torch.int8
+        elif epilogue in (EPI_RESADD_F32, EPI_F32):
+            dt = torch.float32
+        else:
+            dt = torch.float16
+        assert epilogue != EPI_RESADD_F32, "residual epilogue needs an out tensor"
+        out = torch.empty(shape + (n,), dtype=dt, device=a2.device)
+    o2 = out.reshape(-1, n)
+    assert o2.stride(-1) == 1 and o2.shape[0] == a2.shape[0]
+    return out, o2
+
+
+def i8_gemm(a: torch.Tensor, bfmt: int, wpacked: torch.Tensor, wscale: torch.Tensor, n: int,
+            bias: Optional[torch.Tensor] = None, qzeros: Optional[torch.Tensor] = None, epilogue: int = EPI_BIAS,
+            a_scale: float = 1.0, out_scale: float = 0.0, mid_scale: float = 0.0, res_scale: float = 0.0,
+            res: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, cfg: int = 0) -> torch.Tensor:
+    """int8 codes a (..., K) x packed weights (bfmt 0: W8 from w8_repack, 1: GPTQ W4 layout 3)."""
+    _need_cuda(a, wpacked, wscale, bias, qzeros, res)
+    assert a.dtype == torch.int8 and wscale.dtype == torch.float32
+    assert bias is None or bias.dtype == torch.float32
+    k = a.shape[-1]
+    a2 = a.reshape(-1, k)
+    out, o2 = _i8_out(a2, n, epilogue, out, tuple(a.shape[:-1]))
+    r2 = None if res is None else res.reshape(-1, n)
+    status = _lib.load().samq_i8_gemm_cfg(
+        _ptr(a2), a2.stride(0), bfmt, _ptr(wpacked), _ptr(wscale), _ptr(qzeros), _ptr(bias), _ptr(o2), o2.stride(0),
+        _ptr(r2), 0 if r2 is None else r2.stride(0), a2.shape[0], n, k, epilogue, float(a_scale), float(mid_scale),
+        float(res_scale), float(out_scale), cfg, _stream())
+    _lib.check(status, "i8_gemm")
+    return out
+
+
+def w8a8_gemm(a, wpacked, wscale, n, bias=None, epilogue=EPI_Q8, a_scale=1.0, out_scale=0.0, mid_scale=0.0,
+              res_scale=0.0, res=None, out=None):
+    """fq_vit QLinear on int8 codes: ``epilogue(float(sum a w) * a_scale * wscale[n] + bias[n])``."""
+    return i8_gemm(a, _lib.BF_W8, wpacked, wscale, n, bias, None, epilogue, a_scale, out_scale, mid_scale,
+                   res_scale, res, out)
+
+
+def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_scale=1.0, out_scale=0.0,
+              out=None, groupsize=-1):
+    """GPTQ int4 weights (repacked layout 3) x int8 activation codes."""
+    if groupsize not in (-1, a.shape[-1]):
+        raise NotImplementedError("w4a8_gemm: only groupsize -1 (per-channel) is supported with int8 activations")
+    return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out)
+
+
+def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,
+                     rel_pos_w: torch.Tensor, heads: int, window: int, sm_scale: float, s_qkv: float, s_a1: float,
+                     s_a2: float, s_out: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """W8A8 attention on int8 qkv codes (B, H, W, 3C) -> int8 output codes (B, H, W, C)."""
+    _need_cuda(qkv, qkv_bias, rel_pos_h, rel_pos_w)
+    b, h, w, c3 = qkv.shape
+    c = c3 // 3
+    assert qkv.dtype == torch.int8 and qkv.is_contiguous()
+    assert rel_pos_h.dtype == torch.float32 and rel_pos_w.dtype == torch.float32
+    assert qkv_bias is None or qkv_bias.dtype == torch.float32
+    if out is None:
+        out = torch.empty((b, h, w, c), dtype=torch.int8, device=qkv.device)
+    _lib.check(_lib.load().samq_rel_attention_q8(
+        _ptr(qkv), _ptr(qkv_bias), _ptr(rel_pos_h.contiguous()), _ptr(rel_pos_w.contiguous()), _ptr(out), b, h, w,
+        heads, c // heads, window, float(sm_scale), float(s_qkv), float(s_a1), float(s_a2), float(s_out), _stream()),
+        "rel_attention_q8")
     return out

@@ -1,0 +1,348 @@
+"""W8A8 (fq_vit) path: the module mirror on CPU (calibration semantics vs the reference's goldens)
+and the HIP int8 kernels / fused engine on the GPU (vs the CPU oracle F and the goldens).
+
+Tolerances.  The reference sums fp32 products of fake-quant values; the kernels sum the int8
+codes exactly and scale once, so the pre-quantisation values differ by fp32 rounding (~1e-6
+relative) and a value lying that close to a rounding boundary of the next quantiser can land one
+code apart.  Kernel tests therefore require: every code within +-1 of the reference and at most
+a small stated fraction of codes off by one.  Encoder tests state the fraction of output codes
+equal to the golden codes and the max-abs difference in units of the output scale.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fq_ref, sam_ref, synth
+
+
+def _golden_model(golden_dir, tag, img_size):
+    g = np.load(golden_dir / f"fq_vitb_{tag}.npz", allow_pickle=False)
+    meta = json.loads(str(g["meta"]))
+    cfg = synth.encoder_config("vit_b", img_size=img_size)
+    st = {k: v.astype(np.float16).astype(np.float32) for k, v in synth.make_encoder_state(cfg, seed=meta["seed"]).items()}
+    return g, meta, cfg, st
+
+
+def _product_fq(cfg, st, device="cpu"):
+    from samq import fq_vit
+    enc = fq_vit.build_fq_image_encoder("vit_b", img_size=cfg["img_size"])
+    missing, unexpected = enc.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert all("quantizer" in k for k in missing), missing
+    return enc.to(device).eval()
+
+
+# ----------------------------------------------------------------------------- CPU: module mirror
+def test_fq_module_calibration_matches_reference_scales(golden_dir):
+    """Our fq_vit module tree + calibration switches reproduce the reference's 140 activation
+    scales and every per-channel weight scale bit for bit (same torch CPU ops)."""
+    g, meta, cfg, st = _golden_model(golden_dir, "img256", 256)
+    enc = _product_fq(cfg, st)
+    enc.calibrate_with([torch.from_numpy(synth.make_images(1, 256, seed=s)) for s in meta["calib_seeds"]])
+    names = list(g["act_scale_names"])
+    from samq import fq_vit
+    qa = fq_vit.act_quantizers(enc)
+    assert set(qa) == set(names)
+    mine = np.array([float(qa[n].quantizer.scale) for n in names], np.float32)
+    np.testing.assert_array_equal(mine, g["act_scales"])
+    mods = dict(enc.named_modules())
+    for k in g.files:
+        if k.startswith("wscale:"):
+            np.testing.assert_array_equal(mods[k[7:]].quantizer.scale.numpy(), g[k])
+    # quant-mode module graph on CPU (reference semantics, torch ops) == golden codes
+    out = enc.module_forward(torch.from_numpy(synth.make_images(1, 256, seed=meta["test_seed"]))).detach().numpy()
+    np.testing.assert_array_equal(np.round(out / g["out_scale"]), g["codes"].astype(np.float64))
+
+
+def test_fq_quant_encoder_refuses_cpu(golden_dir):
+    g, meta, cfg, st = _golden_model(golden_dir, "img256", 256)
+    enc = _product_fq(cfg, st)
+    from samq import fq_vit
+    fq_vit.calibrate_weights(enc)
+    fq_vit.set_act_scales(enc, dict(zip(g["act_scale_names"], g["act_scales"])))
+    enc.model_quant()
+    with pytest.raises(RuntimeError, match="GPU"):
+        enc(torch.zeros(1, 3, 256, 256))
+
+
+# ----------------------------------------------------------------------------- GPU: kernels
+def _codes_close(out, ref, max_frac, what):
+    out = out.astype(np.int64)
+    ref = ref.astype(np.int64)
+    d = np.abs(out - ref)
+    frac = float((d > 0).mean())
+    assert d.max() <= 1, f"{what}: code off by {d.max()}"
+    assert frac <= max_frac, f"{what}: {frac:.2e} of codes off by one (> {max_frac:.1e})"
+    return frac
+
+
+def _rq(v, s):
+    return np.clip(np.round(v / np.float32(s)), -128, 127)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 84])
+def test_w8a8_gemm_epilogues(cuda, cfg):
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(11 + cfg))
+    m, k, n = 333, 768, 512
+    a = rng.integers(-128, 128, (m, k), dtype=np.int8)
+    w = rng.integers(-128, 128, (n, k), dtype=np.int8)
+    ws = (rng.random(n, dtype=np.float32) * 1e-3 + 1e-4).astype(np.float32)
+    bias = (rng.standard_normal(n, dtype=np.float32) * 0.5).astype(np.float32)
+    a_s = np.float32(0.013)
+    acc = a.astype(np.int64) @ w.astype(np.int64).T
+    y = acc.astype(np.float64) * (np.float64(a_s) * ws.astype(np.float64)) + bias
+    da, dw = torch.from_numpy(a).to(cuda), ops.w8_repack(torch.from_numpy(w).to(cuda))
+    dws, db = torch.from_numpy(ws).to(cuda), torch.from_numpy(bias).to(cuda)
+    f32 = ops.i8_gemm(da, 0, dw, dws, n, db, epilogue=ops.EPI_F32, a_scale=float(a_s), cfg=cfg).cpu().numpy()
+    assert np.abs(f32 - y).max() <= 1e-5 * np.abs(y).max()
+    s_o = np.float32(np.abs(y).max() / 127.5)
+    q = ops.i8_gemm(da, 0, dw, dws, n, db, epilogue=ops.EPI_Q8, a_scale=float(a_s), out_scale=float(s_o), cfg=cfg)
+    _codes_close(q.cpu().numpy(), _rq(y, s_o), 2e-4, "Q8")
+    gl = 0.5 * y * (1 + np.vectorize(__import__("math").erf)(y / np.sqrt(2)))
+    s_g = np.float32(np.abs(gl).max() / 127.5)
+    qg = ops.i8_gemm(da, 0, dw, dws, n, db, epilogue=ops.EPI_Q8_GELU, a_scale=float(a_s), out_scale=float(s_g), cfg=cfg)
+    _codes_close(qg.cpu().numpy(), _rq(gl, s_g), 2e-4, "Q8_GELU")
+    res = rng.integers(-128, 128, (m, n), dtype=np.int8)
+    s_r, s_mid = np.float32(0.02), np.float32(np.abs(y).max() / 127.5)
+    mid = _rq(y, s_mid) * s_mid
+    xr = res.astype(np.float32) * s_r + mid.astype(np.float32)
+    s_x = np.float32(np.abs(xr).max() / 127.5)
+    dres = torch.from_numpy(res).to(cuda)
+    qr = ops.i8_gemm(da, 0, dw, dws, n, db, epilogue=ops.EPI_Q8_RES, a_scale=float(a_s), out_scale=float(s_x),
+                     mid_scale=float(s_mid), res_scale=float(s_r), res=dres, out=dres, cfg=cfg)   # in place
+    _codes_close(qr.cpu().numpy(), _rq(xr, s_x), 5e-4, "Q8_RES")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [0, 81, 82, 83])
+def test_w4a8_gemm_exact_integer(cuda, cfg):
+    """int4 (layout 3, incl. a zero point of 0 -> quirk 4) x int8: integer sums are exact."""
+    from oracle import gptq_pack
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(5 + cfg))
+    m, k, n = 300, 1280, 512
+    w = rng.standard_normal((n, k), dtype=np.float32) * np.float32(0.02)
+    w[7] = np.abs(w[7])
+    fake, s, z = gptq_pack.rtn_quantize_linear(w, -1)
+    qw, qz, sc = gptq_pack.pack_linear(fake, s, z, -1)
+    q = gptq_pack.unpack_qweight(qw).astype(np.int64)            # (K, N)
+    zp = gptq_pack.unpack_zeros(qz).astype(np.int64)[0]          # (N,) decoded nibble + 1
+    a = rng.integers(-128, 128, (m, k), dtype=np.int8)
+    ref = a.astype(np.int64) @ (q - zp[None, :])
+    packed = ops.w4_repack(torch.from_numpy(qw).to(cuda), layout=3)
+    ones = torch.ones(n, dtype=torch.float32, device=cuda)
+    out = ops.i8_gemm(torch.from_numpy(a).to(cuda), 1, packed, ones, n, None, torch.from_numpy(qz).to(cuda),
+                      epilogue=ops.EPI_F32, a_scale=1.0, cfg=cfg)
+    np.testing.assert_array_equal(out.cpu().numpy().astype(np.int64), ref)
+    # scaled fp16 output with bias == activation * int4 dequant (fp32 ref, fp16 output rounding)
+    a_s = np.float32(0.02)
+    bias = (rng.standard_normal(n, dtype=np.float32) * 0.02).astype(np.float32)
+    scf = sc.astype(np.float32).reshape(-1)
+    y = ref.astype(np.float64) * (np.float64(a_s) * scf) + bias
+    o16 = ops.w4a8_gemm(torch.from_numpy(a).to(cuda), packed, torch.from_numpy(scf).to(cuda),
+                        torch.from_numpy(qz).to(cuda), n, torch.from_numpy(bias).to(cuda), ops.EPI_BIAS, float(a_s))
+    assert np.abs(o16.float().cpu().numpy() - y).max() <= 1e-3 * max(1.0, np.abs(y).max())
+
+
+@pytest.mark.gpu
+def test_quantize_and_layernorm_q(cuda):
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(3))
+    x = (rng.standard_normal((517, 768), dtype=np.float32) * 3).astype(np.float32)
+    s = np.float32(0.037)
+    codes = ops.quantize(torch.from_numpy(x).to(cuda), float(s)).cpu().numpy()
+    ref = torch.clamp(torch.round(torch.from_numpy(x) / torch.tensor(s)), -128, 127).numpy()
+    np.testing.assert_array_equal(codes.astype(np.float32), ref)
+    fq = ops.quantize(torch.from_numpy(x).to(cuda), float(s), fake=True).cpu().numpy()
+    np.testing.assert_array_equal(fq, ref * s)
+    tail = ops.quantize(torch.from_numpy(x.reshape(-1)[:1003].copy()).to(cuda), float(s)).cpu().numpy()
+    np.testing.assert_array_equal(tail.astype(np.float32), ref.reshape(-1)[:1003])
+    # LN on int8 codes -> int8 codes (fq_vit norm1 + qact1 / neck LN2d + qacts)
+    g = (1 + 0.1 * rng.standard_normal(768)).astype(np.float32)
+    b = (0.1 * rng.standard_normal(768)).astype(np.float32)
+    xc = codes.astype(np.int8)
+    xf = torch.from_numpy(xc.astype(np.float32) * s)
+    for eps in (1e-6, 1e-5):
+        y = torch.nn.functional.layer_norm(xf, (768,), torch.from_numpy(g), torch.from_numpy(b), eps=eps).numpy()
+        s_o = np.float32(np.abs(y).max() / 127.5)
+        out = ops.layernorm_q(torch.from_numpy(xc).to(cuda), torch.from_numpy(g).to(cuda),
+                              torch.from_numpy(b).to(cuda), eps, in_scale=float(s), out_scale=float(s_o))
+        _codes_close(out.cpu().numpy(), _rq(y, s_o), 1e-3, "layernorm_q")
+        fq32 = ops.layernorm_q(torch.from_numpy(xc).to(cuda), torch.from_numpy(g).to(cuda),
+                               torch.from_numpy(b).to(cuda), eps, in_scale=float(s), out_scale=float(s_o),
+                               out_dtype=torch.float32).cpu().numpy()
+        np.testing.assert_array_equal(fq32, out.cpu().numpy().astype(np.float32) * s_o)
+
+
+def _attn_ref(qkv_codes, bias, relh, relw, heads, window, s_qkv, s1, s2, s_o):
+    """fq_vit Attention core (oracle F semantics) on fake-quant qkv values, with windowing."""
+    b, h, w, c3 = qkv_codes.shape
+    c = c3 // 3
+    d = c // heads
+    qkv = torch.from_numpy(qkv_codes.astype(np.float32) * s_qkv)
+    if window > 0:
+        # pad tokens project the zero-padded LN output: qkv = bias, then attn.qact1
+        pad_val = fq_ref.fake_quant(torch.from_numpy(bias), torch.tensor(s_qkv))
+        hp, wp = -(-h // window) * window, -(-w // window) * window
+        full = pad_val.expand(b, hp, wp, c3).clone()
+        full[:, :h, :w] = qkv
+        qkv, _ = sam_ref.window_partition(full, window)
+    bq, hh, ww, _ = qkv.shape
+    t = qkv.reshape(bq, hh * ww, 3, heads, d).permute(2, 0, 3, 1, 4)
+    q, k, v = t.reshape(3, bq * heads, hh * ww, d).unbind(0)
+    sc = (q * (d ** -0.5)) @ k.transpose(-2, -1)
+    sc = fq_ref.fake_quant(sc, torch.tensor(s1))
+    rh, rw = sam_ref.rel_bias(q.reshape(bq * heads, hh, ww, d), torch.from_numpy(relh), torch.from_numpy(relw), hh, ww)
+    sc = (sc.view(bq * heads, hh, ww, hh, ww) + rh[..., :, None] + rw[..., None, :]).view(bq * heads, hh * ww, hh * ww)
+    sc = fq_ref.fake_quant(sc, torch.tensor(s2))
+    o = (torch.softmax(sc, -1) @ v).view(bq, heads, hh, ww, d).permute(0, 2, 3, 1, 4).reshape(bq, hh, ww, c)
+    if window > 0:
+        o = sam_ref.window_unpartition(o, window, (hp, wp), (h, w))
+    return np.clip(np.round((o / s_o).numpy()), -128, 127)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,hw,window", [(1, 20, 14), (2, 14, 14), (1, 16, 0), (1, 32, 0), (1, 64, 0)])
+def test_rel_attention_q8(cuda, b, hw, window):
+    from samq import ops
+    heads, d = 2 if hw == 64 else 3, 64
+    c = heads * d
+    rng = np.random.Generator(np.random.PCG64(hw + window))
+    qkv = rng.integers(-128, 128, (b, hw, hw, 3 * c), dtype=np.int8)
+    side = window or hw
+    relh = (rng.standard_normal((2 * side - 1, d), dtype=np.float32) * 0.5).astype(np.float32)
+    relw = (rng.standard_normal((2 * side - 1, d), dtype=np.float32) * 0.5).astype(np.float32)
+    bias = (rng.standard_normal(3 * c, dtype=np.float32) * 0.3).astype(np.float32)
+    s_qkv = np.float32(0.02)
+    # score scales chosen like minmax calibration would (max |score| / 127.5)
+    s1, s2, s_o = np.float32(2.0 / 127.5), np.float32(6.0 / 127.5), np.float32(2.6 / 127.5)
+    ref = _attn_ref(qkv, bias, relh, relw, heads, window, s_qkv, s1, s2, s_o)
+    out = ops.rel_attention_q8(torch.from_numpy(qkv).to(cuda), torch.from_numpy(bias).to(cuda),
+                               torch.from_numpy(relh).to(cuda), torch.from_numpy(relw).to(cuda), heads, window,
+                               d ** -0.5, float(s_qkv), float(s1), float(s2), float(s_o))
+    _codes_close(out.cpu().numpy(), ref, 5e-3, f"attention_q8 {b}x{hw} win {window}")
+
+
+# ----------------------------------------------------------------------------- GPU: encoder
+def _gpu_fq(cfg, st, g, device):
+    from samq import fq_vit
+    enc = _product_fq(cfg, st, device)
+    fq_vit.calibrate_weights(enc)
+    fq_vit.set_act_scales(enc, dict(zip(g["act_scale_names"], g["act_scales"])))
+    enc.model_quant()
+    return enc
+
+
+def _cpu_reference_taps(cfg, st, g, img_t):
+    """Our module graph in quant mode on the CPU (== the reference's goldens, see
+    test_fq_module_calibration_matches_reference_scales) with every QAct output recorded."""
+    from samq import fq_vit
+    enc = _gpu_fq(cfg, st, g, "cpu")
+    taps = {}
+    for n, m in fq_vit.act_quantizers(enc).items():
+        m.register_forward_hook(lambda mod, inp, out, n=n: taps.__setitem__(n, out.detach()))
+    enc.module_forward(img_t)
+    return taps
+
+
+@pytest.mark.gpu
+def test_w8a8_stage_local_parity(cuda, golden_dir):
+    """Each fused W8A8 stage fed the reference's own int8 inputs reproduces the reference's output
+    codes (all within +-1, <= 1e-4 of them off by one): LN+qact, qkv GEMM+qact, windowed and global
+    attention (score quantisers, rel-pos, softmax, qact2), proj / lin2 GEMM + qact + residual +
+    qact, lin1 GEMM + GELU + qact.  This is the kernel-level bit parity; the encoder-level
+    statistics follow in test_w8a8_encoder_vs_golden."""
+    from samq import ops
+    g, meta, cfg, st = _golden_model(golden_dir, "img256", 256)
+    img_t = torch.from_numpy(synth.make_images(1, 256, seed=meta["test_seed"]))
+    ref = _cpu_reference_taps(cfg, st, g, img_t)
+    scales = dict(zip(g["act_scale_names"], g["act_scales"]))
+    eng = _gpu_fq(cfg, st, g, cuda).engine()
+    c, gsz = cfg["embed_dim"], 256 // 16
+
+    def codes(n, shape=None):
+        t = torch.round(ref[n] / float(scales[n])).to(torch.int8)
+        return (t if shape is None else t.reshape(shape)).to(cuda).contiguous()
+
+    def check(what, out, n, natural=None):
+        r = ref[n] if natural is None else natural
+        rc = np.round(r.numpy() / scales[n]).reshape(-1)
+        _codes_close(out.cpu().numpy().reshape(-1), rc, 1e-4, what)
+
+    for i in range(cfg["depth"]):
+        bl, pre = eng.blocks[i], f"blocks.{i}."
+        xin_n = "qact1" if i == 0 else f"blocks.{i - 1}.qact4"
+        s_in = float(scales[xin_n])
+        check(pre + "LN1", ops.layernorm_q(codes(xin_n, (-1, c)), *bl["n1"], in_scale=s_in, out_scale=bl["s_ln1"]),
+              pre + "qact1")
+        win = bl["window"]
+        qkv_ref = ref[pre + "attn.qact1"]
+        ao_ref = ref[pre + "attn.qact2"]
+        if win:
+            hp = -(-gsz // win) * win
+            qkv_ref = sam_ref.window_unpartition(qkv_ref.reshape(-1, win, win, 3 * c), win, (hp, hp), (gsz, gsz))
+            ao_ref = sam_ref.window_unpartition(ao_ref, win, (hp, hp), (gsz, gsz))
+        else:
+            qkv_ref = qkv_ref.reshape(1, gsz, gsz, 3 * c)
+        qkv = eng._gemm(codes(pre + "qact1", (-1, c)), bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"])
+        check(pre + "qkv", qkv, pre + "attn.qact1", qkv_ref)
+        qc = torch.round(qkv_ref / float(scales[pre + "attn.qact1"])).to(torch.int8).to(cuda).contiguous()
+        ao = ops.rel_attention_q8(qc, bl["qkv_bias"], bl["relh"], bl["relw"], bl["heads"], win, bl["scale"],
+                                  bl["s_qkv"], bl["s_a1"], bl["s_a2"], bl["s_ao"])
+        check(pre + f"attention (window {win})", ao, pre + "attn.qact2", ao_ref)
+        aoc = torch.round(ao_ref / float(scales[pre + "attn.qact2"])).to(torch.int8).to(cuda).reshape(-1, c)
+        x1 = codes(xin_n, (-1, c))
+        eng._gemm(aoc.contiguous(), bl["proj"], ops.EPI_Q8_RES, bl["s_ao"], bl["s_x1"], mid=bl["s_proj"], res=x1,
+                  res_scale=s_in, out=x1)
+        check(pre + "proj+res", x1, pre + "qact2")
+        check(pre + "LN2", ops.layernorm_q(codes(pre + "qact2", (-1, c)), *bl["n2"], in_scale=bl["s_x1"],
+                                           out_scale=bl["s_ln2"]), pre + "qact3")
+        check(pre + "lin1+gelu", eng._gemm(codes(pre + "qact3", (-1, c)), bl["lin1"], ops.EPI_Q8_GELU, bl["s_ln2"],
+                                           bl["s_h"]), pre + "mlp.qact1")
+        x3 = codes(pre + "qact2", (-1, c))
+        eng._gemm(codes(pre + "mlp.qact1", (-1, 4 * c)), bl["lin2"], ops.EPI_Q8_RES, bl["s_h"], bl["s_x2"],
+                  mid=bl["s_l2"], res=x3, res_scale=bl["s_x1"], out=x3)
+        check(pre + "lin2+res", x3, pre + "qact4")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,img", [("img256", 256), ("img1024", 1024)])
+def test_w8a8_encoder_vs_golden(cuda, golden_dir, tag, img):
+    """Fused HIP W8A8 engine with the reference's calibrated scales vs the reference's output codes.
+
+    A W8A8 fake-quant encoder is chaotic at the code level: evaluating the SAME reference graph in
+    float64 instead of float32 (oracle F, dtype=float64) already changes ~80% of the output codes
+    by a few units (measured: 20.8% equal, mean |dcode| 1.53 at img 256), so no implementation can
+    match the fp32 CPU codes bit for bit end to end (stage-level bit parity is
+    test_w8a8_stage_local_parity).  Stated tolerance: our distance to the reference is at most
+    1.25x the reference's own fp32-vs-fp64 distance (+0.05 codes), cosine similarity >= 0.995,
+    max-abs <= 0.15 x absmax."""
+    g, meta, cfg, st = _golden_model(golden_dir, tag, img)
+    enc = _gpu_fq(cfg, st, g, cuda)
+    img_np = synth.make_images(1, img, seed=meta["test_seed"])
+    out = enc(torch.from_numpy(img_np).to(cuda)).float().cpu().numpy()
+    s_out = float(g["out_scale"])
+    codes = np.round(out / s_out)
+    np.testing.assert_allclose(codes * s_out, out, rtol=0, atol=1e-5 * max(1.0, np.abs(out).max()))
+    ref = g["codes"].astype(np.float64)
+    o64 = fq_ref.FQEncoderOracle(cfg, st, dtype=torch.float64)
+    o64.set_scales(dict(zip(g["act_scale_names"], g["act_scales"])))
+    c64 = np.round(o64(img_np).numpy() / s_out)
+
+    def stats(a, b):
+        d = np.abs(a - b)
+        cos = float((a * b).sum() / np.sqrt((a * a).sum() * (b * b).sum()))
+        return float((d == 0).mean()), float(d.mean()), float(d.max()), cos
+
+    ours, self_ = stats(codes, ref), stats(c64, ref)
+    print(f"\nW8A8 vit_b {img}: ours vs reference: {ours[0] * 100:.2f}% codes equal, mean |dcode| {ours[1]:.3f}, "
+          f"max {ours[2]:.0f}, cos {ours[3]:.5f} | reference fp64 vs fp32: {self_[0] * 100:.2f}% equal, "
+          f"mean {self_[1]:.3f}, max {self_[2]:.0f}, cos {self_[3]:.5f} | ours vs fp64: "
+          f"mean {stats(codes, c64)[1]:.3f}")
+    assert ours[1] <= 1.25 * self_[1] + 0.05
+    assert ours[3] >= 0.995
+    assert ours[2] * s_out <= 0.15 * np.abs(ref).max() * s_out

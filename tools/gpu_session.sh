@@ -21,6 +21,7 @@ run() {  # name, seconds, command...
 for step in "$@"; do
   case $step in
     kernels) run kernels 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rA ;;
+    w8a8)    run w8a8 600 python -m pytest tests/test_w8a8.py -q -m gpu -s -rA ;;
     encoder) run encoder 700 python -m pytest tests/test_gpu_encoder.py -q -m gpu -s -rA ;;
     gpu)     run gputests 900 python -m pytest tests -q -m gpu -s -rA ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
