@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
-"""Benchmark: 1024x1024 images/sec through the W4A16 (GPTQ int4) ViT-H SAM image encoder.
+"""Benchmark: 1024x1024 images/sec through the quantized SAM image encoder.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model vit_h]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--mode w4a16|w4a8|w8a8]
+
+Default (the headline, BASELINE config 3/4): ``--mode w4a16`` = ViT-H GPTQ int4 weights x fp16
+activations.  ``--mode w4a8`` (config 5): ViT-H int4 weights x int8 activations on the int8 MFMA,
+batch 8.  ``--mode w8a8`` (config 2): vit_b fq_vit W8A8, batch 1.
 
 One process per GPU (for N > 1 launched by ``torch.distributed.run``; RANK / LOCAL_RANK /
 WORLD_SIZE / MASTER_* from the env).  A "step" = one encoder forward over the per-GPU batch of
@@ -69,7 +73,70 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
                 avg_launch_us=round(t / n * 1e6, 2))
 
 
-def cpu_baseline(model_name: str):
+PEAK_INT8_TOPS = 5000.0     # MI355X dense int8 MFMA (2x fp16, MI355X_MICROARCH.md)
+
+
+def _time_launches(launches, reps=3):
+    """launches: list of (callable, flops); returns (total seconds, total flops, count)."""
+    stream = torch.cuda.current_stream()
+    records = []
+    for _ in range(reps):
+        for fn, fl in launches:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            records.append((e0, e1, fl))
+    torch.cuda.synchronize()
+    t = sum(e0.elapsed_time(e1) for e0, e1, _ in records) / 1e3
+    return t, sum(f for *_, f in records), len(records)
+
+
+def w4a8_roofline(eng, batch: int):
+    from samq import ops
+    bufs = eng.buffers(batch)
+    rows = bufs["x"].numel() // bufs["x"].shape[-1]
+    launches = []
+    for p in eng.plans:
+        for lin, a, s, out, epi, so in ((p.qkv, "xn8", p.s_qkv, "qkv", ops.EPI_BIAS, 0.0),
+                                        (p.proj, "att8", p.s_proj, "x", ops.EPI_RESADD_F32, 0.0),
+                                        (p.lin1, "xn8", p.s_lin1, "hid8", ops.EPI_Q8_GELU, p.s_lin2),
+                                        (p.lin2, "hid8", p.s_lin2, "x", ops.EPI_RESADD_F32, 0.0)):
+            launches.append((lambda lin=lin, a=a, s=s, out=out, epi=epi, so=so:
+                             lin.forward_w4a8(bufs[a], s, epi, out=bufs[out], out_scale=so),
+                             2.0 * rows * lin.infeatures * lin.outfeatures))
+    t, fl, n = _time_launches(launches)
+    achieved = fl / t / 1e12
+    return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_INT8_TOPS, unit="TFLOP/s",
+                frac=round(achieved / PEAK_INT8_TOPS, 4), traffic=None,
+                kernel="i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)", launches_timed=n,
+                avg_launch_us=round(t / n * 1e6, 2))
+
+
+def w8a8_roofline(eng, batch: int):
+    from samq import ops
+    dev = eng.dev
+    c = eng.embed_dim
+    rows = batch * (eng.enc.img_size // eng.patch) ** 2
+    a = torch.randint(-100, 100, (rows, 4 * c), dtype=torch.int8, device=dev)
+    x = torch.randint(-100, 100, (rows, c), dtype=torch.int8, device=dev)
+    launches = []
+    for bl in eng.blocks:
+        for lw, epi, k in ((bl["qkv"], ops.EPI_Q8, c), (bl["proj"], ops.EPI_Q8_RES, c),
+                           (bl["lin1"], ops.EPI_Q8_GELU, c), (bl["lin2"], ops.EPI_Q8_RES, 4 * c)):
+            res = x if epi == ops.EPI_Q8_RES else None
+            launches.append((lambda lw=lw, epi=epi, k=k, res=res: eng._gemm(a[:, :k], lw, epi, 0.01, 0.05, mid=0.05,
+                                                                         res=res, res_scale=0.05),
+                             2.0 * rows * lw["k"] * lw["n"]))
+    t, fl, n = _time_launches(launches)
+    achieved = fl / t / 1e12
+    return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_INT8_TOPS, unit="TFLOP/s",
+                frac=round(achieved / PEAK_INT8_TOPS, 4), traffic=None,
+                kernel="i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)", launches_timed=n,
+                avg_launch_us=round(t / n * 1e6, 2))
+
+
+def cpu_baseline(model_name: str, mode: str = "w4a16"):
     """Oracle restatement of the reference CPU fake-quant path (fp32 encoder with dequantised
     int4 weights), one 1024x1024 image, rank 0 only."""
     sys.path.insert(0, str(REPO))
@@ -82,13 +149,30 @@ def cpu_baseline(model_name: str):
     st = {}
     for k, shape in _state_shapes(cfg).items():
         st[k] = torch.randn(shape, generator=g) * 0.02
-    o = sam_ref.EncoderOracle(cfg, st)
+    if mode == "w8a8":
+        from oracle import fq_ref
+        o = fq_ref.FQEncoderOracle(cfg, st)
+        qa = ["qact_input", "patch_embed.qact", "qact_pos", "qact1"] + [f"qacts.{i}" for i in range(4)]
+        for i in range(cfg["depth"]):
+            qa += [f"blocks.{i}.{n}" for n in ("qact1", "qact2", "qact3", "qact4", "attn.qact1", "attn.qact2",
+                                                 "attn.qact3", "attn.qact_attn1", "attn.use_rel_pos_qact",
+                                                 "mlp.qact1", "mlp.qact2")]
+        o.set_scales({n: 0.05 for n in qa})
+        what = "fq_vit W8A8 fake-quant op graph (oracle/fq_ref.py)"
+    elif mode == "w4a8":
+        from oracle import w4a8_ref
+        o = w4a8_ref.W4A8EncoderOracle(cfg, st)
+        o.set_scales({n: 0.05 for n in synth.linear_names(cfg)})
+        what = "W4A8 fake-quant op graph (oracle/w4a8_ref.py)"
+    else:
+        o = sam_ref.EncoderOracle(cfg, st)
+        what = "fp32 CPU fake-quant op graph (oracle/sam_ref.py)"
     img = torch.randn(1, 3, 1024, 1024, generator=g)
     t0 = time.perf_counter()
     o(img)
     dt = time.perf_counter() - t0
     return dict(value=round(1.0 / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample=f"1 image, {model_name} fp32 CPU fake-quant op graph (oracle/sam_ref.py), "
+                sample=f"1 image, {model_name} {what}, "
                        f"{dt:.1f} s wall, torch {threads} threads, CPU: {_cpu_model()}")
 
 
@@ -130,30 +214,46 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=0, help="images per GPU (default 4 at N=1, 8 at N>1)")
-    ap.add_argument("--model", default="vit_h")
+    ap.add_argument("--model", default="")
+    ap.add_argument("--mode", default="w4a16", choices=("w4a16", "w4a8", "w8a8"))
     ap.add_argument("--groupsize", type=int, default=-1)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
+    import samq
     from samq import dist as sdist
-    from samq.synthetic import flops_per_image, random_quant_encoder
+    from samq.synthetic import flops_per_image, random_fq_encoder, random_quant_encoder
 
     rank, world = sdist.init_from_env()
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(dev)
-    batch = args.batch or (4 if world == 1 else 8)
+    mode = args.mode
+    model = args.model or ("vit_b" if mode == "w8a8" else "vit_h")
+    batch = args.batch or {"w4a16": 4 if world == 1 else 8, "w4a8": 8, "w8a8": 1}[mode]
 
     t0 = time.time()
-    enc = random_quant_encoder(args.model, args.groupsize, device=dev, init=(rank == 0))
-    nbytes = sdist.broadcast_state(enc, src=0)
+    if mode == "w8a8":
+        # fq_vit W8A8: random weights calibrated on one seeded image (identical on every rank)
+        enc = random_fq_encoder(model, device=dev)
+        nbytes = 0
+    else:
+        enc = random_quant_encoder(model, args.groupsize, device=dev, init=(rank == 0))
+        nbytes = sdist.broadcast_state(enc, src=0)
+        if mode == "w4a8":
+            enc.half()
+            samq.make_act_quant(enc)
+            gcal = torch.Generator(device="cpu").manual_seed(99)
+            cal = torch.randn((1, 3, 1024, 1024), generator=gcal).to(dev, torch.float16)
+            samq.calibrate_act_quant(enc, enc.module_forward, [cal])
     eng = enc.engine()
-    log(f"[rank {rank}] model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB)")
+    log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB)")
 
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    img = torch.randn((batch, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
+    img = torch.randn((batch, 3, 1024, 1024), generator=g, device=dev,
+                      dtype=torch.float32 if mode == "w8a8" else torch.float16)
     if args.no_graph:
         run = lambda: eng(img)  # noqa: E731
     else:
@@ -177,7 +277,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    roof = gemm_roofline(eng, batch)
+    roof = {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, batch)
     fl = flops_per_image(enc)
     total_imgs = world * batch * args.steps
     value = total_imgs / elapsed
@@ -186,10 +286,14 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "img/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": f"SAM {args.model} image encoder W4A16 GPTQ (int4 RTN-packed, "
-                                   f"groupsize {args.groupsize}), {batch} x 1024x1024 images per GPU",
-                       "model": args.model, "global_batch": world * batch, "per_gpu_batch": batch,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": {"w4a16": "fp16", "w4a8": "int8", "w8a8": "int8"}[mode], "data": "synthetic",
+            "config": {"workload": {
+                "w4a16": f"SAM {model} image encoder W4A16 GPTQ (int4 RTN-packed, groupsize {args.groupsize})",
+                "w4a8": f"SAM {model} image encoder W4A8 (GPTQ int4 weights, int8 minmax activations)",
+                "w8a8": f"SAM {model} image encoder W8A8 fq_vit (int8 per-channel weights, int8 activations)",
+            }[mode] + f", {batch} x 1024x1024 images per GPU", "mode": mode,
+                       "model": model, "global_batch": world * batch, "per_gpu_batch": batch,
                        "seq_len": 4096, "parallelism": f"image-parallel x{world} (weights RCCL-broadcast once)",
                        "graph": not args.no_graph},
             "roofline": roof,
@@ -198,7 +302,7 @@ def main():
                     "frac_of_int8_peak": round(e2e_tflops / (2 * PEAK_FP16_TFLOPS), 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.model)
+            line["cpu_baseline"] = cpu_baseline(model, mode)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -19,11 +19,14 @@ from . import _lib, ops, quant_linear, fused_attention  # noqa: F401
 from .build_sam import Sam, build_sam, build_sam_vit_b, build_sam_vit_h, build_sam_vit_l, sam_model_registry  # noqa
 from .fused_attention import QuantAttention, make_quant_attn
 from .modeling import ImageEncoderViT
-from .quant_linear import QuantLinear, make_quant, matmul4, triton_matmul4  # noqa: F401
+from .quant_linear import (QuantLinear, calibrate_act_quant, make_act_quant, make_quant, matmul4,  # noqa: F401
+                           triton_matmul4)
+from . import fq_vit  # noqa: F401
 
 __all__ = [
     "load_quant", "autotune_warmup", "QuantLinear", "make_quant", "matmul4", "triton_matmul4",
     "QuantAttention", "make_quant_attn", "ImageEncoderViT", "Sam", "sam_model_registry",
+    "make_act_quant", "calibrate_act_quant", "fq_vit",
 ]
 
 

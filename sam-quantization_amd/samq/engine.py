@@ -30,7 +30,7 @@ from .quant_linear import QuantLinear
 
 class _BlockPlan:
     __slots__ = ("ln1_w", "ln1_b", "ln1_eps", "qkv", "proj", "relh", "relw", "heads", "window", "scale",
-                 "ln2_w", "ln2_b", "ln2_eps", "lin1", "lin2", "qkv_bias")
+                 "ln2_w", "ln2_b", "ln2_eps", "lin1", "lin2", "qkv_bias", "s_qkv", "s_proj", "s_lin1", "s_lin2")
 
 
 class EncoderEngine:
@@ -63,7 +63,17 @@ class EncoderEngine:
             p.relh, p.relw = self._tables(attn, side)
             p.ln1_w, p.ln1_b, p.ln1_eps = self._ln(blk.norm1)
             p.ln2_w, p.ln2_b, p.ln2_eps = self._ln(blk.norm2)
+            p.s_qkv, p.s_proj, p.s_lin1, p.s_lin2 = (lin.act_scale() for lin in (qkv, proj, blk.mlp.lin1, blk.mlp.lin2))
             self.plans.append(p)
+        # W4A8 when every block Linear has a calibrated int8 input quantiser in quant mode
+        flags = [s is not None for p in self.plans for s in (p.s_qkv, p.s_proj, p.s_lin1, p.s_lin2)]
+        if any(flags) and not all(flags):
+            raise NotImplementedError("W4A8 engine: either all or none of the block Linears quantise their input")
+        self.w4a8 = bool(flags) and all(flags)
+        if self.w4a8:
+            for p in self.plans:
+                for lin in (p.qkv, p.proj, p.lin1, p.lin2):
+                    lin.prepare_w4a8()
         pe = enc.patch_embed.proj
         self.patch = pe.kernel_size[0]
         self.pe_w = pe.weight.detach().reshape(pe.weight.shape[0], -1).to(torch.float16).contiguous()
@@ -81,7 +91,7 @@ class EncoderEngine:
     # ---------------------------------------------------------------- helpers
     @staticmethod
     def _make_key(enc):
-        return tuple((id(m), getattr(m, "qweight", None) is not None and m.qweight._version)
+        return tuple((id(m), getattr(m, "qweight", None) is not None and m.qweight._version, m.act_scale())
                      for m in enc.modules() if isinstance(m, QuantLinear))
 
     def valid_for(self, enc) -> bool:
@@ -114,6 +124,11 @@ class EncoderEngine:
                 att=torch.empty((b, g, g, c), dtype=torch.float16, device=dev),
                 hid=torch.empty((b, g, g, hid), dtype=torch.float16, device=dev),
             )
+            if self.w4a8:
+                bufs.update(xn8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
+                            att8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
+                            hid8=torch.empty((b, g, g, hid), dtype=torch.int8, device=dev))
+                del bufs["xn"], bufs["hid"]
             self._bufs[b] = bufs
         return bufs
 
@@ -129,7 +144,22 @@ class EncoderEngine:
             y = y + self.pos
         x32.copy_(y)
 
+    def block_w4a8(self, p: _BlockPlan, bufs) -> None:
+        """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded
+        into LN / the GELU epilogue / a quantiser after the attention), int8 MFMA GEMMs."""
+        x, xn8, qkv, att, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att"], bufs["att8"], bufs["hid8"]
+        ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
+        p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
+        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        ops.quantize(att, p.s_proj, out=att8)
+        p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
+        ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
+        p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
+        p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
+
     def block(self, p: _BlockPlan, bufs) -> None:
+        if self.w4a8:
+            return self.block_w4a8(p, bufs)
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
         ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn)
         p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)

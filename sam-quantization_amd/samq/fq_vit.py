@@ -782,3 +782,18 @@ class W8A8Engine:
         y3 = ops.layernorm_q(y2, self.ln_n3[0], self.ln_n3[1], self.ln_n3[2], in_scale=sq[2], out_scale=sq[3],
                              out_dtype=torch.float32)
         return y3.view(b, gh, gw, oc).permute(0, 3, 1, 2)
+
+    __call__ = forward
+
+    def capture(self, img_static: torch.Tensor):
+        """Record one forward into a HIP graph; returns ``(graph, out)`` (see EncoderEngine.capture)."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.forward(img_static)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = self.forward(img_static)
+        return graph, out

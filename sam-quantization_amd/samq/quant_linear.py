@@ -60,6 +60,9 @@ class QuantLinear(nn.Module):
             self.register_parameter("bias", None)
         self.register_buffer("wpacked", None, persistent=False)
         self._packed_from = None
+        # W4A8: an fq_vit QAct on the input (make_act_quant); None = W4A16
+        self.act_quant = None
+        self._w4a8 = None
 
     # -- kernel-side weight layout ------------------------------------------------------
     def prepare(self) -> torch.Tensor:
@@ -70,12 +73,48 @@ class QuantLinear(nn.Module):
             self._packed_from = key
         return self.wpacked
 
+    def prepare_w4a8(self) -> dict:
+        """Kernel-side buffers of the W4A8 GEMM: int4 weights in the int8-MFMA fragment order
+        (repack layout 3), f32 per-channel scales and bias."""
+        if self.groupsize != self.infeatures:
+            raise NotImplementedError("W4A8 needs per-channel weights (groupsize -1)")
+        key = (self.qweight.data_ptr(), self.qweight.device, self.qweight._version, self.scales._version)
+        if self._w4a8 is None or self._w4a8["key"] != key:
+            self._w4a8 = dict(key=key, packed=ops.w4_repack(self.qweight, layout=3),
+                              scale=self.scales.float().reshape(-1).contiguous(),
+                              bias=None if self.bias is None else self.bias.float().contiguous())
+        return self._w4a8
+
+    def act_scale(self) -> Optional[float]:
+        """The calibrated int8 input scale in quant mode, else None (W4A16)."""
+        aq = self.act_quant
+        if aq is None or not aq.quant or aq.calibrate:
+            return None
+        sc = aq.quantizer.scale
+        if sc is None or sc.numel() != 1:
+            raise RuntimeError("QuantLinear.act_quant is not calibrated (layer-wise scale expected)")
+        return float(sc.reshape(-1)[0])
+
+    def forward_w4a8(self, codes: torch.Tensor, a_scale: float, epilogue: int, out: Optional[torch.Tensor] = None,
+                     out_scale: float = 0.0) -> torch.Tensor:
+        """int8 input codes (scale ``a_scale``) x int4 weights on the int8 MFMA."""
+        w = self.prepare_w4a8()
+        return ops.w4a8_gemm(codes, w["packed"], w["scale"], self.qzeros, self.outfeatures, w["bias"], epilogue,
+                             a_scale, out_scale, out=out)
+
     def forward_epilogue(self, x: torch.Tensor, epilogue: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         assert x.shape[-1] == self.qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
         return ops.w4a16_gemm(x, self.prepare(), self.scales, self.qzeros, self.bias, self.outfeatures,
                               self.groupsize, epilogue, out=out)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.act_quant is not None:
+            s = self.act_scale()
+            if s is not None:
+                codes = ops.quantize(x.contiguous(), s)
+                return self.forward_w4a8(codes, s, ops.EPI_BIAS)
+            if self.act_quant.calibrate:
+                self.act_quant(x.float())          # observer pass (fq_vit calibrate mode)
         return self.forward_epilogue(x, ops.EPI_BIAS)
 
     def extra_repr(self) -> str:
@@ -117,3 +156,37 @@ def autotune_warmup(model: nn.Module):
         return run
 
     return (make(m) for m in seen.values())
+
+
+# ----------------------------------------------------------------------------- W4A8
+def make_act_quant(model: nn.Module, cfg=None) -> int:
+    """Attach an fq_vit ``QAct`` (int8 symmetric, layer-wise minmax, ``fq_vit/models/ptq/layers.py:
+    203-242``) to the input of every ``QuantLinear``: the W4A8 composition of SURVEY.md §8c.
+    Calibrate with ``calibrate_act_quant``; returns the number of quantisers attached."""
+    from .fq_vit import QAct, sam_w8a8_config
+    cfg = cfg or sam_w8a8_config()
+    n = 0
+    for m in model.modules():
+        if isinstance(m, QuantLinear):
+            dev = m.qweight.device
+            m.act_quant = QAct(bit_type=cfg.BIT_TYPE_A, calibration_mode=cfg.CALIBRATION_MODE_A,
+                               observer_str=cfg.OBSERVER_A, quantizer_str=cfg.QUANTIZER_A).to(dev)
+            n += 1
+    return n
+
+
+@torch.no_grad()
+def calibrate_act_quant(model: nn.Module, run, images) -> None:
+    """fq_vit calibration sequence (``test_quant.py:284-294``) over the W4A8 input quantisers:
+    ``run(img)`` must execute the MODULE forward (e.g. ``encoder.module_forward``)."""
+    aqs = [m.act_quant for m in model.modules() if isinstance(m, QuantLinear) and m.act_quant is not None]
+    images = list(images)
+    for q in aqs:
+        q.quant, q.calibrate, q.last_calibrate = False, True, False
+    for i, img in enumerate(images):
+        if i == len(images) - 1:
+            for q in aqs:
+                q.last_calibrate = True
+        run(img)
+    for q in aqs:
+        q.calibrate, q.last_calibrate, q.quant = False, False, True

@@ -1,0 +1,107 @@
+"""W4A8 path (config 5): GPTQ int4 weights x fq_vit int8 activations on the int8 MFMA.
+
+Oracle: ``oracle.w4a8_ref.W4A8EncoderOracle`` -- the composition prescribed by SURVEY.md §8c
+(oracle G1's int4 fake-quant encoder + an fq_vit int8 QAct on every QuantLinear input); its two
+halves are pinned by the G1 and fq_vit goldens (test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import synth
+from oracle.w4a8_ref import W4A8EncoderOracle
+from _encoder_helpers import oracle_vith, product_encoder
+
+
+def _oracle(depth, seed, img_size=1024, name="vit_h", global_idx=None):
+    cfg, st, names, q = oracle_vith(depth, seed, name=name, img_size=img_size, global_idx=global_idx)
+    from oracle import sam_ref
+    lw = sam_ref.quantized_linear_weights(q, names, -1)
+    lb = {n: q[n + ".bias"].astype(np.float32) for n in names}
+    return cfg, st, names, q, W4A8EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb)
+
+
+def test_w4a8_oracle_composition_cpu():
+    """The composition's calibration observes exactly the Linear inputs (4 per block) and its
+    quant-mode output stays close to the W4 (G1) float model (int8 activation noise only)."""
+    cfg, st, names, q, o = _oracle(2, 31, img_size=256, name="vit_b", global_idx=(1,))
+    imgs = [synth.make_images(1, 256, seed=s) for s in (1, 2)]
+    o.calibrate(imgs)
+    assert sorted(o.scales) == sorted(names)
+    assert all(float(v) > 0 for v in o.scales.values())
+    x = synth.make_images(1, 256, seed=3)
+    yq = o(x).numpy()
+    o.mode = "float"
+    yf = o(x).numpy()
+    err = np.abs(yq - yf).max() / np.abs(yf).max()
+    assert 1e-4 < err < 0.2, err
+
+
+def test_make_act_quant_host(tmp_path):
+    """make_act_quant attaches one QAct per QuantLinear; calibrated scales live in the state dict."""
+    import samq
+    from samq.build_sam import build_image_encoder
+    enc = build_image_encoder(768, 2, 12, [1], img_size=256)
+    samq.make_quant(enc, 4, -1)
+    assert samq.make_act_quant(enc) == 8
+    for m in enc.modules():
+        if isinstance(m, samq.QuantLinear):
+            m.act_quant.observer.update(torch.randn(4, m.infeatures))
+            m.act_quant.quantizer.update_quantization_params()
+            m.act_quant.quant = True
+    sd = enc.state_dict()
+    keys = [k for k in sd if k.endswith("act_quant.quantizer.scale")]
+    assert len(keys) == 8
+    enc2 = build_image_encoder(768, 2, 12, [1], img_size=256)
+    samq.make_quant(enc2, 4, -1)
+    samq.make_act_quant(enc2)
+    enc2.load_state_dict(sd)
+    for k in keys:
+        assert torch.equal(enc2.state_dict()[k], sd[k])
+
+
+@pytest.mark.gpu
+def test_w4a8_vith_vs_oracle(cuda):
+    """ViT-H (2 blocks: windowed + global) W4A8 engine vs the W4A8 oracle fed the same scales.
+
+    The int8 activation quantisers make the output sensitive to arithmetic differences upstream
+    of them: the engine keeps the W4A16 path's fp16 attention, so a few % of the proj-input codes
+    sit one step away from the fp32 oracle's (measured per op in tools/debug_w4a8.py; the int4
+    GEMMs themselves are exact, test_w8a8.py::test_w4a8_gemm_exact_integer).  Stated tolerance
+    (statistical): the distance to the W4A8 oracle is at most 1.5x the size of the int8
+    activation noise itself (oracle W4A8 vs oracle W4A16), in max-abs and in mean-abs."""
+    import samq
+    cfg, st, names, q, o = _oracle(2, 7, global_idx=(1,))
+    enc = product_encoder(cfg, st, names, q, -1, cuda).half()   # the reference runs model.half()
+    samq.make_act_quant(enc)
+    calib = [synth.make_images(1, 1024, seed=s) for s in (1, 2)]
+    samq.calibrate_act_quant(enc, lambda im: enc.module_forward(torch.from_numpy(im).to(cuda).half()), calib)
+    o.calibrate(calib)
+    mine = {n: float(m.act_quant.quantizer.scale) for n, m in enc.named_modules()
+            if isinstance(m, samq.QuantLinear)}
+    names_q = {n.replace("qkv_proj", "qkv").replace("o_proj", "proj"): v for n, v in mine.items()}
+    rel = max(abs(names_q[k] / float(o.scales[k]) - 1) for k in o.scales)
+    print(f"\nGPU calibration vs oracle scales: max rel diff {rel:.2e}")
+    assert rel < 2e-2
+    # like-for-like: the product takes the oracle's scales (as a calibrated checkpoint would)
+    for n, m in enc.named_modules():
+        if isinstance(m, samq.QuantLinear):
+            key = n.replace("qkv_proj", "qkv").replace("o_proj", "proj")
+            m.act_quant.quantizer.scale.fill_(float(o.scales[key]))
+    x = synth.make_images(1, 1024, seed=9)
+    eng = enc.engine()
+    assert eng.w4a8
+    out = eng(torch.from_numpy(x).to(cuda).half(), out_dtype=torch.float32).cpu().numpy()
+    ref = o(x).numpy()
+    err, mean = np.abs(out - ref).max(), np.abs(out - ref).mean()
+    o.mode = "float"
+    w4 = o(x).numpy()
+    nmax, nmean = np.abs(ref - w4).max(), np.abs(ref - w4).mean()
+    print(f"W4A8 ViT-H 2 blocks vs oracle: max-abs {err:.3e} mean-abs {mean:.3e} | int8-activation noise "
+          f"(oracle W4A8 vs W4A16): max-abs {nmax:.3e} mean-abs {nmean:.3e} | vs oracle W4A16: "
+          f"max-abs {np.abs(out - w4).max():.3e}")
+    assert err <= 1.5 * nmax and mean <= 1.5 * nmean
+    # module path (QuantLinear.forward -> quantize + W4A8 GEMM) agrees with the engine
+    with torch.no_grad():
+        mod = enc.module_forward(torch.from_numpy(x).to(cuda).half()).float().cpu().numpy()
+    assert np.abs(mod - ref).max() <= 1.5 * nmax and np.abs(mod - ref).mean() <= 1.5 * nmean

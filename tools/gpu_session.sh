@@ -22,10 +22,13 @@ for step in "$@"; do
   case $step in
     kernels) run kernels 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rA ;;
     w8a8)    run w8a8 600 python -m pytest tests/test_w8a8.py -q -m gpu -s -rA ;;
+    w4a8)    run w4a8 600 python -m pytest tests/test_w4a8.py -q -m gpu -s -rA ;;
     encoder) run encoder 700 python -m pytest tests/test_gpu_encoder.py -q -m gpu -s -rA ;;
     gpu)     run gputests 900 python -m pytest tests -q -m gpu -s -rA ;;
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 500 python bench.py --steps 20 --warmup 5 ;;
+    bench48) run bench_w4a8 600 python bench.py --mode w4a8 --steps 10 --warmup 3 ;;
+    bench88) run bench_w8a8 600 python bench.py --mode w8a8 --steps 20 --warmup 5 ;;
     benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
