@@ -134,15 +134,21 @@ class EncoderEngine:
 
     # ---------------------------------------------------------------- stages
     def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
+        """Patch embedding as im2col + GEMM, one GEMM per image so that an image's result does
+        not depend on the batch it is in (the vendor GEMM picks its algorithm by M).  W4A8 computes
+        it in fp32: its first int8 quantiser sits right behind it."""
         b = img.shape[0]
         p, g = self.patch, self.grid
-        cols = img.to(torch.float16).reshape(b, -1, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(b * g * g, -1)
-        y = torch.matmul(cols, self.pe_w.t()).float().view(b, g, g, -1)
-        if self.pe_b is not None:
-            y = y + self.pe_b
-        if self.pos is not None:
-            y = y + self.pos
-        x32.copy_(y)
+        dt = torch.float32 if self.w4a8 else torch.float16
+        w = self.pe_w.to(dt) if self.w4a8 else self.pe_w
+        cols = img.to(dt).reshape(b, -1, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(b, g * g, -1)
+        for i in range(b):
+            y = torch.matmul(cols[i], w.t()).float().view(g, g, -1)
+            if self.pe_b is not None:
+                y = y + self.pe_b
+            if self.pos is not None:
+                y = y + self.pos[0]
+            x32[i].copy_(y)
 
     def block_w4a8(self, p: _BlockPlan, bufs) -> None:
         """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded
@@ -172,10 +178,11 @@ class EncoderEngine:
     def neck(self, x32: torch.Tensor, out_dtype) -> torch.Tensor:
         b, g = x32.shape[0], self.grid
         oc = self.out_chans
-        y = torch.matmul(x32.view(-1, self.C).to(torch.float16), self.n0_w.t())           # 1x1 conv
+        x16 = x32.view(b, -1, self.C).to(torch.float16)
+        y = torch.stack([torch.matmul(x16[i], self.n0_w.t()) for i in range(b)])          # 1x1 conv (per image)
         y = ops.layernorm(y.view(b, g, g, oc), *self.n1[:2], eps=self.n1[2])                # LN2d (NHWC rows)
         cols = F.unfold(y.permute(0, 3, 1, 2), kernel_size=3, padding=1)                    # (b, oc*9, g*g)
-        y = torch.matmul(cols.transpose(1, 2), self.n2_w.t())                                # 3x3 conv
+        y = torch.stack([torch.matmul(cols[i].t(), self.n2_w.t()) for i in range(b)])       # 3x3 conv
         y = ops.layernorm(y.reshape(b, g, g, oc).contiguous(), *self.n3[:2], eps=self.n3[2],
                           out_dtype=torch.float32)
         return y.permute(0, 3, 1, 2).to(out_dtype)
