@@ -43,6 +43,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(pattern: str, profile: str):
+    """HBM bytes per launch of the kernels matching ``pattern`` (dispatch-weighted average) from a
+    committed rocprofv3 PMC summary (tools/pmc_traffic.sh -> profiles/*.json), or None."""
+    f = REPO / "profiles" / profile
+    if not f.exists():
+        return None, None
+    d = json.loads(f.read_text())
+    tot = n = 0
+    for k, v in d["kernels"].items():
+        if pattern in k and v.get("hbm_bytes_avg"):
+            tot += v["hbm_bytes_avg"] * v["dispatches"]
+            n += v["dispatches"]
+    return (round(tot / n) if n else None), f"profiles/{profile}: " + d["source"]
+
+
 def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
     """Average duration of every W4A16 GEMM launch of one forward, measured with HIP events on
     the launch stream; achieved = algorithmic FLOPs (2*M*N*K per launch) / duration."""
@@ -67,9 +82,17 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
     flops = sum(f for *_, f in records)
     n = len(records)
     achieved = flops / t / 1e12
+    # algorithmic bytes per launch (A f16 in, packed int4 W, output f16 or f32 read-modify-write)
+    alg = []
+    for p in eng.plans:
+        for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
+            alg.append(rows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + rows * lin.outfeatures * out_b)
+    traffic, src = pmc_traffic("w4a16_gemm_v3", "r1_pmc_traffic_w4a16.json") if bufs_batch == 4 else (None, None)
     return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_FP16_TFLOPS, unit="TFLOP/s",
-                frac=round(achieved / PEAK_FP16_TFLOPS, 4), traffic=None,
-                kernel="w4a16_gemm_kernel (all 4 ViT-H projection shapes)", launches_timed=n,
+                frac=round(achieved / PEAK_FP16_TFLOPS, 4), traffic=traffic,
+                traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
+                algorithmic_bytes_per_launch=round(sum(alg) / len(alg)),
+                kernel="w4a16_gemm_v3 (all 4 ViT-H projection shapes)", launches_timed=n,
                 avg_launch_us=round(t / n * 1e6, 2))
 
 

@@ -318,8 +318,10 @@ void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
   constexpr int STAGE = A_BYTES + NB * 1024;
   constexpr int STAGES = 3;
   static_assert(TM >= 1 && TN >= 1 && NPW <= 15, "bad tile");
+  constexpr int EP_BYTES = 32 * WN * 4;                // epilogue: one 32-row slice per wave, f32
+  constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
 
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -457,8 +459,6 @@ void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
     csc[t] = GROUPED ? 1.0f : (float)scales[col[t]];
     cb[t] = bias ? (float)bias[col[t]] : 0.0f;
   }
-  constexpr int EP_BYTES = 32 * WN * 4;                // one 32-row slice of the wave tile, f32
-  static_assert(NW * EP_BYTES <= STAGES * STAGE, "epilogue staging does not fit the LDS ring");
   __syncthreads();                                      // every wave is done with the ring
   float* ep = (float*)(smem + wave * EP_BYTES);
   const int row_base = m0 + wm * WM;
@@ -744,6 +744,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
     case 26: return launch_v3<64, 64, 2, 2, EPI, GR>(a, st);
     case 27: return launch_v3<128, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
     case 28: return launch_v3<256, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
+    // 320-column tiles: ViT-H N in {1280, 3840, 5120} and M = 128*B give whole waves of tiles
+    case 29: return launch_v3<128, 320, 2, 5, EPI, GR>(a, st);
+    case 30: return launch_v3<256, 320, 2, 5, EPI, GR>(a, st);
+    case 31: return launch_v3<128, 320, 1, 5, EPI, GR>(a, st);
     // v4 (16x16x32, packed LAYOUT 2)
     case 41: return launch_v4<128, 256, 2, 4, EPI, GR>(a, st);
     case 42: return launch_v4<256, 256, 2, 4, EPI, GR>(a, st);
@@ -779,7 +783,8 @@ static int cfg_bn(int cfg) {
                  case 5: return 32; case 6: return 256; case 7: return 256; case 8: return 128;
                  case 9: return 256; case 11: return 256; case 21: return 256; case 22: return 256;
                  case 23: return 128; case 24: return 128; case 25: return 256; case 26: return 64;
-                 case 27: return 256; case 28: return 256; case 41: return 256; case 42: return 256;
+                 case 27: return 256; case 28: return 256; case 29: return 320; case 30: return 320;
+                 case 31: return 320; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
                  default: return 0; }
 }
@@ -834,10 +839,10 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
   const bool vec_ok = ((uintptr_t)C & 15) == 0 && ldc % 8 == 0;
   if (cfg <= 0) {
     cfg = pick_cfg(M, N);
-    if (!vec_ok && cfg >= 21 && cfg <= 28) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
+    if (!vec_ok && cfg >= 21 && cfg <= 31) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
   }
   SAMQ_REQUIRE(cfg_bn(cfg) > 0 && N % cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a16_gemm: N not divisible by tile");
-  SAMQ_REQUIRE(vec_ok || cfg < 21 || cfg > 28, SAMQ_ERR_INVALID,
+  SAMQ_REQUIRE(vec_ok || cfg < 21 || cfg > 31, SAMQ_ERR_INVALID,
                "w4a16_gemm: this tile config needs a 16-byte aligned C with ldc % 8 == 0");
   GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
              (const _Float16*)bias, C, ldc, M, N, K, groupsize};
