@@ -92,3 +92,38 @@ def make_images(batch: int, img_size: int = 1024, seed: int = 1) -> np.ndarray:
     input (reference ``gptq4sam_infer.py:64``)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     return rng.standard_normal((batch, 3, img_size, img_size), dtype=np.float32)
+
+
+def make_decoder_state(shapes: dict, seed: int = 300) -> dict:
+    """Seeded weights for the SAM prompt encoder + mask decoder, given ``{key: shape}`` (taken
+    from the module's own ``state_dict``, so the reference and our modules receive the same
+    tensors).  Keys are visited in sorted order.  Embeddings and the Fourier matrix ~ N(0, 1);
+    LayerNorm weight 1 + N(0, 0.1), bias N(0, 0.1); other biases N(0, 0.02); matrices and conv
+    kernels N(0, 1/fan_in)."""
+    import re
+    unit = re.compile(r"(point_embeddings\.\d+|not_a_point_embed|no_mask_embed|iou_token|mask_tokens)\.weight$"
+                      r"|positional_encoding_gaussian_matrix$")
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = {}
+    for k in sorted(shapes):
+        shape = tuple(shapes[k])
+        z = rng.standard_normal(shape).astype(np.float32)
+        ln = len(shape) == 1 and len(tuple(shapes.get(k.rsplit(".", 1)[0] + ".weight", ()))) == 1
+        if unit.search(k):
+            out[k] = z
+        elif ln and k.endswith(".weight"):
+            out[k] = (1.0 + 0.1 * z).astype(np.float32)
+        elif len(shape) == 1:
+            out[k] = ((0.1 if ln else 0.02) * z).astype(np.float32)
+        else:
+            out[k] = (z / np.sqrt(float(np.prod(shape[1:])))).astype(np.float32)
+    return out
+
+
+DECODER_PROMPTS = [
+    dict(points=[[512.0, 512.0]], labels=[1]),
+    dict(points=[[200.0, 300.0]], labels=[1]),
+    dict(points=[[700.0, 150.0], [650.0, 220.0]], labels=[1, 0]),
+    dict(points=[[120.0, 880.0], [900.0, 900.0], [500.0, 640.0]], labels=[1, 1, 0]),
+    dict(box=[300.0, 260.0, 760.0, 700.0]),
+]

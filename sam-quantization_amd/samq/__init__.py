@@ -22,11 +22,12 @@ from .modeling import ImageEncoderViT
 from .quant_linear import (QuantLinear, calibrate_act_quant, make_act_quant, make_quant, matmul4,  # noqa: F401
                            triton_matmul4)
 from . import fq_vit  # noqa: F401
+from .sam_decoder import ResizeLongestSide, SamPredictor, mask_iou  # noqa: F401
 
 __all__ = [
     "load_quant", "autotune_warmup", "QuantLinear", "make_quant", "matmul4", "triton_matmul4",
     "QuantAttention", "make_quant_attn", "ImageEncoderViT", "Sam", "sam_model_registry",
-    "make_act_quant", "calibrate_act_quant", "fq_vit",
+    "make_act_quant", "calibrate_act_quant", "fq_vit", "SamPredictor", "ResizeLongestSide", "mask_iou",
 ]
 
 

@@ -19,6 +19,10 @@ What it does (all on CPU, seeded, numpy PCG64 weights from ``oracle.synth``):
                          the reference-packed int4 weights decoded (oracle G1).
 * ``encoder_vith32.npz`` -- the same for the full 32-block ViT-H (fp16-stored output) plus a
                          sha256 of every reference-packed buffer of the model.
+* ``masks_vith32.npz`` -- reference ``PromptEncoder`` + ``MaskDecoder`` (seeded weights,
+                         ``oracle.synth.make_decoder_state``) on the reference encoder output of
+                         ``encoder_vith32.npz`` for the prompts ``oracle.synth.DECODER_PROMPTS``:
+                         low-res mask logits + IoU predictions (single- and multi-mask).
 * ``fq_vitb.npz``     -- reference fq_vit W8A8 ``ImageEncoderViT`` (vit_b dims, img 256 and
                          1024): calibrate on 2 seeded images (minmax, int8), then quant forward;
                          every QAct scale + weight scales + output codes.
@@ -310,6 +314,43 @@ def make_fq(img_size: int, tag: str):
                                              test_seed=23, torch=torch.__version__)))
 
 
+def make_masks():
+    """Reference prompt encoder + mask decoder on the golden ViT-H embedding (mask-IoU report)."""
+    from segment_anything.modeling.prompt_encoder import PromptEncoder
+    from segment_anything.modeling.mask_decoder import MaskDecoder
+    from segment_anything.modeling.transformer import TwoWayTransformer
+    torch.manual_seed(0)
+    pe = PromptEncoder(embed_dim=256, image_embedding_size=(64, 64), input_image_size=(1024, 1024), mask_in_chans=16)
+    md = MaskDecoder(num_multimask_outputs=3, transformer=TwoWayTransformer(depth=2, embedding_dim=256, mlp_dim=2048,
+                                                                            num_heads=8),
+                     transformer_dim=256, iou_head_depth=3, iou_head_hidden_dim=256)
+    shapes = {f"prompt_encoder.{k}": v.shape for k, v in pe.state_dict().items()}
+    shapes.update({f"mask_decoder.{k}": v.shape for k, v in md.state_dict().items()})
+    st = synth.make_decoder_state(shapes)
+    pe.load_state_dict({k[len("prompt_encoder."):]: torch.from_numpy(v) for k, v in st.items()
+                        if k.startswith("prompt_encoder.")})
+    md.load_state_dict({k[len("mask_decoder."):]: torch.from_numpy(v) for k, v in st.items()
+                        if k.startswith("mask_decoder.")})
+    pe.eval(), md.eval()
+    emb = torch.from_numpy(np.load(HERE / "encoder_vith32.npz")["out"].astype(np.float32))
+    res = {}
+    with torch.no_grad():
+        for i, pr in enumerate(synth.DECODER_PROMPTS):
+            pts = None
+            if "points" in pr:
+                pts = (torch.tensor([pr["points"]], dtype=torch.float32), torch.tensor([pr["labels"]], dtype=torch.int64))
+            box = torch.tensor([pr["box"]], dtype=torch.float32) if "box" in pr else None
+            sparse, dense = pe(points=pts, boxes=box, masks=None)
+            for mm in (False, True):
+                low, iou = md(image_embeddings=emb, image_pe=pe.get_dense_pe(), sparse_prompt_embeddings=sparse,
+                              dense_prompt_embeddings=dense, multimask_output=mm)
+                res[f"low_{i}_{int(mm)}"] = low.numpy().astype(np.float16)
+                res[f"iou_{i}_{int(mm)}"] = iou.numpy().astype(np.float32)
+    np.savez_compressed(HERE / "masks_vith32.npz", **res,
+                        meta=json.dumps(dict(decoder_seed=300, prompts=synth.DECODER_PROMPTS, torch=torch.__version__)))
+    print("masks:", {k: v.shape for k, v in res.items() if k.startswith("low_")})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
@@ -336,6 +377,8 @@ def main():
             make_fq(1024, "img1024")
     if want("enc32") and not args.skip_full:
         make_encoder(R, 32)
+    if want("masks"):
+        make_masks()
 
 
 if __name__ == "__main__":
