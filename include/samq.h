@@ -124,6 +124,11 @@ int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked
 #define SAMQ_Q_OUT_FQ 2
 int samq_quantize(const void* x, void* y, int64_t n, float scale, int flags, hipStream_t stream);
 
+/* Gated-MLP activation: out f16[i] = silu(gate[i]) * up[i] (f32 inputs).  With two
+ * samq_w4a16_gemm(..., SAMQ_EPI_F32) calls it replaces triton_llama_mlp_4 /
+ * llama_mlp_fused_4_kernel (gptq_triton/fused_mlp.py:391-477, 230-388). */
+int samq_silu_mul(const float* gate, const float* up, void* out, int64_t n, hipStream_t stream);
+
 /* ---------------------------------------------------------------- normalisation */
 
 /* y[r,:] = LayerNorm(x[r,:]) * gamma + beta over C channels (row stride C), f32 statistics.

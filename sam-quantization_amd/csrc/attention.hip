@@ -53,11 +53,23 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  // one v_max3_f32; fmaxf on MFMA results otherwise gets canonicalising v_max copies
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+// ds_read_b64_tr_b16 through inline asm: the intrinsic form carries no alias information, so the
+// compiler treats it as possibly reading the in-flight LDS-DMA ring and drains vmcnt(0) before it
+// (killing the K/V prefetch).  The asm form is invisible to that analysis; the caller waits
+// lgkmcnt itself (lds_wait below, which also orders the MFMAs after the wait).
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)((const SAMQ_LDS char*)p);
+}
+__device__ __forceinline__ half4_t ds_read_tr16(uint32_t addr) {
+  half4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
   return r;
+}
+
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  // NOT inline asm: the hazard recognizer does not pad an asm VALU read of a fresh MFMA result,
+  // which then reads stale accumulator lanes at random (nondeterministic scores).
+  return fmaxf(fmaxf(a, b), c);
 }
 
 template <int D, int SP, int QT, int NW, bool RESIDENT, bool PRECOMP, int RS = 16, int SC = 0>
@@ -334,20 +346,30 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
     // ---- O^T += V^T . P^T  (V^T fragments by hardware-transposed LDS reads of row-major V)
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
-      if (SP == 16) {
+      if constexpr (SP == 16) {
         const char* a0 = vb + ((4 * g + trow) * D + d * 16 + tcol) * 2;
         const half4_t va = __builtin_bit_cast(
             half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0)));
 #pragma unroll
         for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x16f16(va, pb16[t], o[t][d], 0, 0, 0);
       } else {
+        constexpr int NS = SP / 32;
+        half4_t lo[NS], hi[NS];
+        const uint32_t vaddr = lds_addr(vb + ((4 * g + trow) * D + d * 16 + tcol) * 2);
 #pragma unroll
-        for (int s = 0; s < SP / 32; ++s) {
-          const char* a0 = vb + ((32 * s + 4 * g + trow) * D + d * 16 + tcol) * 2;
-          const char* a1 = a0 + 16 * D * 2;
-          const half4_t lo = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0)));
-          const half4_t hi = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a1)));
-          const half8_t va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        for (int s = 0; s < NS; ++s) {
+          lo[s] = ds_read_tr16(vaddr + (32 * s) * D * 2);
+          hi[s] = ds_read_tr16(vaddr + (32 * s + 16) * D * 2);
+        }
+        if constexpr (NS == 2) {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]));
+        } else {
+#pragma unroll
+          for (int s = 0; s < NS; ++s) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[s]), "+v"(hi[s]));
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          const half8_t va = {lo[s][0], lo[s][1], lo[s][2], lo[s][3], hi[s][0], hi[s][1], hi[s][2], hi[s][3]};
 #pragma unroll
           for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][s], o[t][d], 0, 0, 0);
         }

@@ -74,3 +74,27 @@ extern "C" int samq_quantize(const void* x, void* y, int64_t n, float scale, int
   SAMQ_LAUNCH_CHECK("quantize launch");
   return SAMQ_OK;
 }
+
+// ------------------------------------------------------------------ gated MLP activation
+// out = silu(gate) * up (f32 in, f16 out): the activation / product of the reference's fused
+// LLaMA MLP kernel (gptq_triton/fused_mlp.py:230-388, silu :386-388), whose two int4 GEMMs run
+// as samq_w4a16_gemm with the f32 epilogue.
+namespace samq {
+__global__ __launch_bounds__(256) void silu_mul_kernel(const float* __restrict__ g, const float* __restrict__ u,
+                                                       _Float16* __restrict__ out, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float x = g[i];
+    out[i] = (_Float16)(x / (1.0f + expf(-x)) * u[i]);
+  }
+}
+}  // namespace samq
+
+extern "C" int samq_silu_mul(const float* gate, const float* up, void* out, int64_t n, hipStream_t stream) {
+  SAMQ_REQUIRE(gate && up && out, SAMQ_ERR_INVALID, "silu_mul: null pointer");
+  if (n <= 0) return SAMQ_OK;
+  const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);
+  hipLaunchKernelGGL(samq::silu_mul_kernel, dim3(blocks), dim3(256), 0, stream, gate, up, (_Float16*)out, n);
+  SAMQ_LAUNCH_CHECK("silu_mul launch");
+  return SAMQ_OK;
+}

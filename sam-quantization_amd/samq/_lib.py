@@ -58,6 +58,7 @@ SIGNATURES = {
     "samq_i8_gemm_cfg": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
                                 _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "samq_quantize": (_i32, [_vp, _vp, _i64, _f32, _i32, _vp]),
+    "samq_silu_mul": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
     "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),
     "samq_rel_attention": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp]),

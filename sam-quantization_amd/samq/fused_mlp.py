@@ -1,0 +1,95 @@
+"""``gptq_triton.fused_mlp`` API on the HIP kernels (API parity).
+
+The reference fuses ``silu(A . Wgate) * (A . Wup)`` for LLaMA MLPs (``fused_mlp.py``:
+``make_fused_mlp`` ``:13-27``, ``autotune_warmup`` ``:30-71``, ``QuantLlamaMLP`` ``:74-112``,
+``llama_mlp_fused_4_kernel`` ``:230-383``, ``triton_llama_mlp_4`` ``:391-477``).  SAM has no such
+MLP (its ``make_fused_mlp`` even references an undefined ``LlamaMLP``); this module keeps the
+names, arguments, buffers and asserts so code written against it runs: two int4 GEMMs with the
+f32 epilogue (exact integer weights, fp32 accumulate, G1 numerics) and one HIP ``silu * up``
+pass.  Biases of gate/up are ignored, as in the reference kernel.
+"""
+from __future__ import annotations
+
+import functools
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+
+
+def triton_llama_mlp_4(groupsize: int, a: torch.Tensor, gate_qweight: torch.Tensor, gate_scales: torch.Tensor,
+                       gate_qzeros: torch.Tensor, up_qweight: torch.Tensor, up_scales: torch.Tensor,
+                       up_qzeros: torch.Tensor) -> torch.Tensor:
+    """``silu(gate(a)) * up(a)``, a (..., K) fp16 -> (..., N) fp16 (reference ``:391-477``)."""
+    assert (gate_qweight.shape == up_qweight.shape and gate_scales.shape == up_scales.shape
+            and gate_qzeros.shape == up_qzeros.shape), "All weights must have the same shape"
+    assert a.shape[-1] == gate_qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
+    assert a.is_contiguous(), "A must be contiguous"
+    k, n = a.shape[-1], gate_qweight.shape[1]
+    assert k % 128 == 0, "K must be a multiple of 16, 32, 64, and 128"
+    assert n % 256 == 0, "N must be a multiple of 16, 32, 64, 128, and 256"
+    gs = k if groupsize == -1 else groupsize
+    assert gs % 128 == 0, "groupsize must be a multiple of 32, 64, and 128"
+    gs = -1 if gs == k else gs
+    x = a.view(-1, k)
+    g = ops.w4a16_gemm(x, ops.w4_repack(gate_qweight), gate_scales, gate_qzeros, None, n, gs, ops.EPI_F32)
+    u = ops.w4a16_gemm(x, ops.w4_repack(up_qweight), up_scales, up_qzeros, None, n, gs, ops.EPI_F32)
+    c = torch.empty((x.shape[0], n), dtype=torch.float16, device=a.device)
+    _lib.check(_lib.load().samq_silu_mul(g.data_ptr(), u.data_ptr(), c.data_ptr(), c.numel(), ops._stream()),
+               "silu_mul")
+    return c.view(a.shape[:-1] + (n,))
+
+
+llama_mlp_4 = triton_llama_mlp_4
+
+
+class QuantLlamaMLP(nn.Module):
+    """``down_proj(silu(gate_proj(x)) * up_proj(x))`` with only the gate/up packed buffers kept
+    (reference ``:74-112``)."""
+
+    def __init__(self, gate_proj, down_proj, up_proj):
+        super().__init__()
+        assert gate_proj.groupsize == up_proj.groupsize
+        self.register_buffer("gate_proj_qweight", gate_proj.qweight)
+        self.register_buffer("gate_proj_scales", gate_proj.scales)
+        self.register_buffer("gate_proj_qzeros", gate_proj.qzeros)
+        self.register_buffer("up_proj_qweight", up_proj.qweight)
+        self.register_buffer("up_proj_scales", up_proj.scales)
+        self.register_buffer("up_proj_qzeros", up_proj.qzeros)
+        self.groupsize = gate_proj.groupsize
+        self.infeatures = gate_proj.infeatures
+        self.outfeatures = down_proj.outfeatures
+        self.down_proj = down_proj
+
+    def forward(self, x):
+        gs = -1 if self.groupsize == self.infeatures else self.groupsize
+        return self.down_proj(triton_llama_mlp_4(gs, x, self.gate_proj_qweight, self.gate_proj_scales,
+                                                 self.gate_proj_qzeros, self.up_proj_qweight, self.up_proj_scales,
+                                                 self.up_proj_qzeros))
+
+
+def make_fused_mlp(m: nn.Module, parent_name: str = "") -> nn.Module:
+    """Replace every LLaMA-style MLP (class named ``LlamaMLP`` with gate/up/down ``QuantLinear``)
+    by ``QuantLlamaMLP`` (reference ``:13-27``)."""
+    if type(m).__name__ == "LlamaMLP" and all(hasattr(m, a) for a in ("gate_proj", "up_proj", "down_proj")):
+        return QuantLlamaMLP(m.gate_proj, m.down_proj, m.up_proj)
+    for name, child in m.named_children():
+        new = make_fused_mlp(child, parent_name=f"{parent_name}.{name}")
+        if isinstance(new, QuantLlamaMLP):
+            setattr(m, name, new)
+    return m
+
+
+def autotune_warmup(model: nn.Module):
+    """One warm-up call per unique K (reference ``:30-71``); there is no autotuner."""
+    mods = {m.infeatures: m for m in model.modules() if isinstance(m, QuantLlamaMLP)}
+    print(f"FusedMLP Warmup: Found {len(mods)} unique K values.")
+
+    def run(mrows, mod):
+        a = torch.randn(1, mrows, mod.infeatures, dtype=torch.float16, device=mod.gate_proj_qweight.device)
+        gs = -1 if mod.groupsize == mod.infeatures else mod.groupsize
+        triton_llama_mlp_4(gs, a, mod.gate_proj_qweight, mod.gate_proj_scales, mod.gate_proj_qzeros,
+                           mod.up_proj_qweight, mod.up_proj_scales, mod.up_proj_qzeros)
+
+    return (functools.partial(run, mod=m) for m in mods.values())
