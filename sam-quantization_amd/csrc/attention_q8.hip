@@ -33,6 +33,7 @@ struct AttnQ8Params {
   int8_t* out;              // [B, H, W, C] codes
   int B, H, W, heads, C, S, window, nwh, nww, L;
   float qk_scale, s_qkv, s_a1, s_a2, s_out;
+  float inv_a1, inv_a2, k2;   // 1/s_a1, 1/s_a2, s_a2*log2(e)
 };
 
 typedef int int4v __attribute__((ext_vector_type(4)));
@@ -44,7 +45,9 @@ __device__ __forceinline__ float aq8(float v, float s) {
 constexpr int QD = 64;       // head dim (vit_b)
 constexpr int KPITCH = 80;   // K row pitch in LDS (bytes): conflict-free 16-byte fragment reads
 
-template <bool RESIDENT, int NWQ, int KC, int MAXS>
+// ROW64: global attention over a 64-wide grid -- a 64-key chunk is exactly one key row, so the
+// height term is one value per chunk and the width term a fixed per-lane set (registers).
+template <bool RESIDENT, int NWQ, int KC, int MAXS, bool ROW64 = false>
 __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params p) {
   constexpr int NBUF = RESIDENT ? 1 : 2;
   constexpr int VTP = KC + 8;                    // V^T row pitch (halves)
@@ -177,6 +180,18 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
   for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
   const float* rhq = &rh_lds[wave][ql * (MAXS + 1)];
   const float* rwq = &rw_lds[wave][ql * (MAXS + 1)];
+  float rwr[4][4];
+  if constexpr (ROW64) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // this wave's rel terms are in LDS
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rwr[bb][i] = rwq[bb * 16 + 4 * g + i];
+  }
+  // Score quantisers by reciprocal multiply: the pre-quantisation values already differ from the
+  // reference's by fp32 summation order, so a correctly rounded division buys no parity here
+  // (stage-level code agreement is tested, test_w8a8_stage_local_parity).
+  const float inv1 = p.inv_a1, inv2 = p.inv_a2, sa1 = p.s_a1;
 
   if (RESIDENT) {
     for (int c0 = 0; c0 < L; c0 += KC) stage(c0, 0);   // KC >= L: one pass
@@ -192,6 +207,8 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
     // ---- S^T block scores
     float c2[4][4];
     float cmax = -INFINITY;
+    float rh_row = 0.f;
+    if constexpr (ROW64) rh_row = rhq[ch];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
       const int4v kf = *(const int4v*)(&k_lds[buf][(koff + bb * 16 + ql) * KPITCH + g * 16]);
@@ -199,15 +216,23 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
       const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = ch * 64 + bb * 16 + 4 * g + i;
-        float c = -INFINITY;
-        if (key < L) {
-          int kh, kw;
-          tok(key, kh, kw);
+        float c;
+        if constexpr (ROW64) {
           const float v = (float)st[i] * p.qk_scale;
-          const float v1 = aq8(v, p.s_a1) * p.s_a1;
-          const float t = (v1 + rhq[kh]) + rwq[kw];
-          c = aq8(t, p.s_a2);
+          const float v1 = fminf(fmaxf(__builtin_rintf(v * inv1), -128.f), 127.f) * sa1;
+          const float t = (v1 + rh_row) + rwr[bb][i];
+          c = fminf(fmaxf(__builtin_rintf(t * inv2), -128.f), 127.f);
+        } else {
+          const int key = ch * 64 + bb * 16 + 4 * g + i;
+          c = -INFINITY;
+          if (key < L) {
+            int kh, kw;
+            tok(key, kh, kw);
+            const float v = (float)st[i] * p.qk_scale;
+            const float v1 = fminf(fmaxf(__builtin_rintf(v * inv1), -128.f), 127.f) * sa1;
+            const float t = (v1 + rhq[kh]) + rwq[kw];
+            c = fminf(fmaxf(__builtin_rintf(t * inv2), -128.f), 127.f);
+          }
         }
         c2[bb][i] = c;
         cmax = fmaxf(cmax, c);
@@ -216,19 +241,20 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
     cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
     cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
     if (cmax > m) {
-      const float alpha = m == -INFINITY ? 0.f : expf(m * p.s_a2 - cmax * p.s_a2);
+      const float alpha = m == -INFINITY ? 0.f : exp2f((m - cmax) * p.k2);
       lsum *= alpha;
 #pragma unroll
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       m = cmax;
     }
-    const float ms = m * p.s_a2;
     float (&pr)[4][4] = c2;   // probabilities overwrite the score codes in place
+    // exp(s_a2 * (c - m)) with c, m integer codes (exact difference); exp2 of a pre-scaled
+    // argument is within a few ulps of the reference's exp(x - max x)
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float pv = c2[bb][i] == -INFINITY ? 0.f : expf(c2[bb][i] * p.s_a2 - ms);
+        const float pv = c2[bb][i] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((c2[bb][i] - m) * p.k2);
         pr[bb][i] = pv;
         lsum += pv;
       }
@@ -294,6 +320,7 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
   // (q * scale) . k with q = c_q * s_qkv, k = c_k * s_qkv  (fq_vit image_encoder.py:455)
   p.qk_scale = (s_qkv * sm_scale) * s_qkv;
   p.s_qkv = s_qkv; p.s_a1 = s_a1; p.s_a2 = s_a2; p.s_out = s_out;
+  p.inv_a1 = 1.0f / s_a1; p.inv_a2 = 1.0f / s_a2; p.k2 = s_a2 * 1.4426950408889634f;
   if (window > 0) {
     SAMQ_REQUIRE(window <= 16, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: window must be <= 16");
     p.S = window; p.window = window;
@@ -309,7 +336,10 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.S = H; p.window = 0; p.nwh = p.nww = 1; p.L = H * W;
     constexpr int NWQ = 4;
     const dim3 grid(B, heads, (p.L + 16 * NWQ - 1) / (16 * NWQ));
-    hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64>), grid, dim3(64 * NWQ), 0, stream, p);
+    if (H == 64)
+      hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, true>), grid, dim3(64 * NWQ), 0, stream, p);
+    else
+      hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, false>), grid, dim3(64 * NWQ), 0, stream, p);
   }
   SAMQ_LAUNCH_CHECK("rel_attention_q8 launch");
   return SAMQ_OK;
