@@ -1,13 +1,15 @@
-"""Producer side of the GPTQ int4 checkpoint format (RTN subset).
+"""Producer side of the GPTQ int4 checkpoint format, on the GPU.
 
 * ``Quantizer``      -- asymmetric per-channel min/max parameters (reference ``gptq.py:200-299``,
                         ``perchannel=True, sym=False``; ``mse`` grid search not used by the SAM scripts);
+* ``GPTQ``           -- Hessian accumulation + the blockwise optimal-brain-quantiser update
+                        (reference ``gptq.py:15-171``), in fp32 torch on the layer's device;
+* ``sam_sequential`` -- the reference's block-by-block calibration of the SAM encoder
+                        (``gptq4sam.py:280-431``, true-sequential groups qkv / proj / lin1+lin2);
 * ``pack_linear``    -- bit-identical to the reference's packing (``gptq4sam.py:434-497``),
                         vectorised in torch so it runs on the GPU in milliseconds per layer;
-* ``quantize_rtn``   -- round-to-nearest quantisation of every encoder Linear -> QuantLinear;
+* ``quantize_rtn`` / ``quantize_gptq`` -- RTN or GPTQ weights of every encoder Linear -> QuantLinear;
 * ``save_quant``     -- ``model.pt`` + ``quant_config.json`` exactly as ``gptq4sam.py:651-663`` writes.
-
-The Hessian-based GPTQ update (``gptq.py:62-171``) is the remaining part of row f3.
 """
 from __future__ import annotations
 
@@ -41,6 +43,129 @@ class Quantizer:
     def quantize(self, w, scale, zero):
         q = torch.clamp(torch.round(w / scale) + zero, 0, self.maxq)
         return scale * (q - zero)
+
+
+class GPTQ:
+    """Second-order weight quantisation of one ``nn.Linear`` (reference ``gptq.py:15-171``).
+
+    ``add_batch`` keeps H = 2/n sum x x^T as a running mean where, as in the reference's SAM
+    variant, every call counts as ONE sample whatever its batch (``gptq.py:33-34``).
+    ``fasterquant`` inverts the damped Hessian through Cholesky factors and quantises column by
+    column inside blocks of ``blocksize``, pushing each column's scaled error onto the columns
+    not yet quantised; group parameters are taken from the error-updated weights at each group
+    start.  The layer's weight is replaced by the fake-quantised one; returns ``(scale, zero)``
+    of shape (rows, groups).
+    """
+
+    def __init__(self, layer: nn.Module, bits: int = 4):
+        self.layer = layer
+        w = layer.weight.data
+        self.rows, self.columns = w.shape[0], w[0].numel()
+        self.dev = w.device
+        self.H = torch.zeros((self.columns, self.columns), device=self.dev, dtype=torch.float32)
+        self.nsamples = 0
+        self.quantizer = Quantizer(bits)
+
+    def add_batch(self, inp: torch.Tensor, out=None) -> None:
+        x = inp.reshape(-1, inp.shape[-1]).t().float()          # (columns, tokens)
+        self.H *= self.nsamples / (self.nsamples + 1)
+        self.nsamples += 1
+        x = math.sqrt(2.0 / self.nsamples) * x
+        self.H += x @ x.t()
+
+    @torch.no_grad()
+    def fasterquant(self, blocksize: int = 128, percdamp: float = 0.01, groupsize: int = -1,
+                    actorder: bool = False):
+        W = self.layer.weight.data.clone().reshape(self.rows, -1).float()
+        qz = self.quantizer
+        scale, zero = qz.find_params(W)
+        H = self.H
+        self.H = None
+        dead = torch.diagonal(H) == 0
+        H[dead, dead] = 1.0
+        W[:, dead] = 0.0
+        perm = None
+        if actorder:
+            perm = torch.argsort(torch.diagonal(H), descending=True)
+            W, H = W[:, perm], H[perm][:, perm]
+        idx = torch.arange(self.columns, device=self.dev)
+        H[idx, idx] += percdamp * torch.mean(torch.diagonal(H))
+        L = torch.linalg.cholesky(H)
+        Hinv = torch.linalg.cholesky(torch.cholesky_inverse(L), upper=True)
+        Q = torch.zeros_like(W)
+        scales, zeros = [], []
+        for i1 in range(0, self.columns, blocksize):
+            i2 = min(i1 + blocksize, self.columns)
+            W1 = W[:, i1:i2].clone()
+            Err1 = torch.zeros_like(W1)
+            Hinv1 = Hinv[i1:i2, i1:i2]
+            for i in range(i2 - i1):
+                col = i1 + i
+                if groupsize != -1 and col % groupsize == 0:
+                    # the reference reads the OUTER W here: columns of the current block as of the
+                    # block start, later columns as of the last block update (gptq.py:113-117)
+                    scale, zero = qz.find_params(W[:, col:col + groupsize])
+                    scales.append(scale)
+                    zeros.append(zero)
+                w = W1[:, i]
+                q = qz.quantize(w, scale, zero)
+                Q[:, col] = q
+                err = (w - q) / Hinv1[i, i]
+                W1[:, i:] -= err[:, None] * Hinv1[i, i:][None, :]
+                Err1[:, i] = err
+            W[:, i2:] -= Err1 @ Hinv[i1:i2, i2:]
+        if perm is not None:
+            Q = Q[:, torch.argsort(perm)]
+        self.layer.weight.data = Q.reshape(self.layer.weight.shape).to(self.layer.weight.dtype)
+        if not scales:
+            scales, zeros = [scale], [zero]
+        return torch.stack(scales, 1), torch.stack(zeros, 1)
+
+
+@torch.no_grad()
+def sam_sequential(encoder: nn.Module, images, groupsize: int = -1, percdamp: float = 0.01,
+                   act_order: bool = False, true_sequential: bool = True, bits: int = 4) -> dict:
+    """GPTQ-quantise every block Linear of a float SAM encoder, block by block, on calibration
+    ``images`` (reference ``gptq4sam.py:280-431``).  Returns ``{name: (scale, zero)}``; the
+    Linear weights are replaced by their fake-quantised values (pack with ``pack_gptq``)."""
+    inps = []
+    for img in images:
+        x = encoder.patch_embed(img)
+        if encoder.pos_embed is not None:
+            x = x + encoder.pos_embed
+        inps.append(x)
+    groups = [["attn.qkv"], ["attn.proj"], ["mlp.lin1", "mlp.lin2"]] if true_sequential else None
+    params = {}
+    for bi, blk in enumerate(encoder.blocks):
+        full = {n: m for n, m in blk.named_modules() if isinstance(m, nn.Linear)}
+        for names in (groups or [list(full)]):
+            g = {n: GPTQ(full[n], bits) for n in names}
+            hooks = [full[n].register_forward_hook(lambda m, i, o, n=n: g[n].add_batch(i[0].data))
+                     for n in names]
+            for x in inps:
+                blk(x)
+            for h in hooks:
+                h.remove()
+            for n in names:
+                params[f"blocks.{bi}.{n}"] = g[n].fasterquant(percdamp=percdamp, groupsize=groupsize,
+                                                              actorder=act_order)
+        inps = [blk(x) for x in inps]
+    return params
+
+
+@torch.no_grad()
+def pack_gptq(encoder: nn.Module, params: dict, groupsize: int = -1, bits: int = 4) -> nn.Module:
+    """``sam_pack`` (reference ``gptq4sam.py:434-451``): swap the calibrated Linears for packed
+    ``QuantLinear`` (bit-identical packing of the fake-quantised weights and their scale / zero)."""
+    dense = {n: m for n, m in encoder.named_modules() if isinstance(m, nn.Linear) and n in params}
+    make_quant(encoder, bits, groupsize)
+    for name, m in encoder.named_modules():
+        if isinstance(m, QuantLinear) and name in dense:
+            lin = dense[name]
+            m.to(lin.weight.device)
+            s, z = params[name]
+            pack_linear(m, lin.weight.detach().float(), s, z, None if lin.bias is None else lin.bias.detach())
+    return encoder
 
 
 def rtn(w: torch.Tensor, groupsize: int = -1, bits: int = 4):

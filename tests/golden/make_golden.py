@@ -23,6 +23,9 @@ What it does (all on CPU, seeded, numpy PCG64 weights from ``oracle.synth``):
                          ``oracle.synth.make_decoder_state``) on the reference encoder output of
                          ``encoder_vith32.npz`` for the prompts ``oracle.synth.DECODER_PROMPTS``:
                          low-res mask logits + IoU predictions (single- and multi-mask).
+* ``gptq_layer.npz``  -- reference ``GPTQ.add_batch`` / ``fasterquant`` (``gptq.py:15-171``) on one
+                         seeded Linear + 4 activation batches: fake-quant weights, scales, zeros
+                         for groupsize -1 / 128 with act_order off / on.
 * ``fq_vitb.npz``     -- reference fq_vit W8A8 ``ImageEncoderViT`` (vit_b dims, img 256 and
                          1024): calibrate on 2 seeded images (minmax, int8), then quant forward;
                          every QAct scale + weight scales + output codes.
@@ -314,6 +317,35 @@ def make_fq(img_size: int, tag: str):
                                              test_seed=23, torch=torch.__version__)))
 
 
+def make_gptq():
+    """Reference ``GPTQ`` (``gptq.py:15-171``) on one seeded Linear + calibration activations
+    (CPU, fp32): fake-quant weights, scales, zeros for groupsize -1 / 128, act_order off / on."""
+    import gptq as ref_gptq
+    torch.cuda.synchronize = lambda *a, **k: None
+    rng = np.random.Generator(np.random.PCG64(77))
+    k, n = 256, 96
+    w = (rng.standard_normal((n, k)) * 0.05).astype(np.float32)
+    xs = [(rng.standard_normal((3, 50, k)) * np.linspace(0.2, 2.0, k)).astype(np.float32) for _ in range(4)]
+    xs[0][..., 5] = 0.0   # a column with a zero Hessian diagonal is impossible with 4 batches; keep dead=False
+    res = dict(w=w, **{f"x{i}": x for i, x in enumerate(xs)})
+    for gs in (-1, 128):
+        for act in (False, True):
+            lin = torch.nn.Linear(k, n, bias=False)
+            lin.weight.data = torch.from_numpy(w.copy())
+            g = ref_gptq.GPTQ(lin)
+            g.quantizer = ref_gptq.Quantizer()
+            g.quantizer.configure(4, perchannel=True, sym=False, mse=False)
+            for x in xs:
+                g.add_batch(torch.from_numpy(x), None)
+            scale, zero = g.fasterquant(percdamp=0.01, groupsize=gs, actorder=act)
+            tag = f"g{gs}_a{int(act)}"
+            res[f"q_{tag}"] = lin.weight.data.numpy().copy()
+            res[f"scale_{tag}"] = scale.numpy()
+            res[f"zero_{tag}"] = zero.numpy()
+    np.savez_compressed(HERE / "gptq_layer.npz", **res)
+    print("gptq:", {k_: v.shape for k_, v in res.items()})
+
+
 def make_masks():
     """Reference prompt encoder + mask decoder on the golden ViT-H embedding (mask-IoU report)."""
     from segment_anything.modeling.prompt_encoder import PromptEncoder
@@ -379,6 +411,8 @@ def main():
         make_encoder(R, 32)
     if want("masks"):
         make_masks()
+    if want("gptq"):
+        make_gptq()
 
 
 if __name__ == "__main__":
