@@ -397,6 +397,360 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   }
 }
 
+// ------------------------------------------------------------------ windowed attention, persistent
+// The 14x14-window blocks (28 of 32 in ViT-H) as a persistent kernel: one workgroup per CU walks
+// its share of the (window, head) items with the NEXT item's K/V already streaming into the
+// second LDS buffer (LDS-DMA) and its Q into registers while the current item computes, so the
+// HBM stream and the MFMA/VALU work overlap inside one CU.  Per item, everything is local to
+// the window and the VALU work per score is cut to max3/sub/exp/cvt:
+//  * the whole score s[q,k] = q.k*scale + TH[q,kh] + TW[q,kw] (log2 domain) comes out of the
+//    MFMAs: S^T = K'.Q'^T on 16x16x32 with TW as the C input, and TH carried by 16 extra
+//    contraction dims -- K' rows get a one-hot of their key row (DMA'd from a constant table
+//    next to the K data), Q' rows get TH[q, 0..15] in fp16 (the reference also rounds rel_h to
+//    fp16, fused_attention.py:46-80); for D = 80 these are the zero-padded dims 80..95 of the
+//    third k-step, so TH costs no MFMA at all;
+//  * one exact softmax over the window's 196 keys (no online rescale); the two masked slots of
+//    each 16-slot key row are -inf in the C input;
+//  * O^T += V^T . P^T on 16x16x32 with two key rows per MFMA (k order [row 2p: 4g..4g+3 |
+//    row 2p+1: 4g..4g+3], the score registers' own layout; V^T by ds_read_b64_tr_b16), and the
+//    softmax denominator as one more MFMA against an all-ones A operand (sum of the same fp16
+//    P that multiplies V);
+//  * the rel-pos tables (shared by every window and head) sit in LDS for the whole kernel.
+// Items are numbered so the 32 workgroups of one XCD take the 16 heads of the same two windows
+// at a time (the cache lines shared by adjacent heads' K/V slices then land in one L2).
+struct OneHot16 { uint16_t v[16 * 16]; };
+constexpr OneHot16 make_onehot16() {
+  OneHot16 o{};
+  for (int r = 0; r < 16; ++r) o.v[r * 16 + r] = 0x3C00;   // fp16 1.0 on the diagonal
+  return o;
+}
+__device__ __attribute__((aligned(16))) OneHot16 g_onehot16 = make_onehot16();
+
+template <int D>
+__global__ __launch_bounds__(64 * 7, 1) void win_attention_kernel(AttnParams p, int items) {
+  constexpr int S = 14, NW = 7, QT = 2;
+  constexpr int KS = 3;                         // k32 steps of Q'.K'^T: D + 16 TH dims <= 96
+  constexpr int DT = D / 16;
+  constexpr int D8 = D / 8;
+  constexpr int KCH = D8 + 2;                   // 16-byte chunks per K' row (data + one-hot)
+  constexpr int KROW = KCH * 16;                // K' row pitch (bytes)
+  constexpr int GTH = (D - 64) / 8;             // first lane group holding TH dims in k-step 2
+  constexpr int RKEYS = S * S + 16 - S;         // 196 keys + slack for the last row's 16-slot tile
+  constexpr int KC = RKEYS * KCH, VC = RKEYS * D8;
+  constexpr int NI = (KC + VC + 64 * NW - 1) / (64 * NW);
+  constexpr int BUFB = NI * NW * 1024;
+  constexpr int TAB = (2 * S - 1) * D;          // elements per rel-pos table
+  constexpr int TABP = TAB + 32;                // + slack: k-step-2 reads past the last row
+  constexpr int TH16_BYTES = NW * QT * 16 * 32;
+  constexpr int SMEM = 2 * TABP * 2 + TH16_BYTES + 2 * BUFB;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(D == 64 || D == 80, "head dim");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  _Float16* tab_h = (_Float16*)smem;
+  _Float16* tab_w = tab_h + TABP;
+  char* th16 = smem + 2 * TABP * 2;
+  char* bufs = th16 + TH16_BYTES;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int ql = lane & 15;
+  const int g = lane >> 4;
+  const int C = p.C;
+  const int64_t ts = p.tok_stride;
+  const float qscale = p.scale * LOG2E;
+  const bool qin2 = 64 + 8 * g < D;             // lane holds real q dims in k-step 2
+  const bool thl = g == GTH || g == GTH + 1;    // lane holds TH dims in k-step 2
+
+  // rel-pos tables -> LDS (once per workgroup); the slack is zeroed
+  for (int i = tid; i < 2 * TABP / 8; i += 64 * NW) {
+    const int which = i >= TABP / 8;
+    const int j = which ? i - TABP / 8 : i;
+    half8_t v = {};
+    if (8 * j < TAB) v = *(const half8_t*)((which ? p.relw : p.relh) + 8 * j);
+    *(half8_t*)((which ? tab_w : tab_h) + 8 * j) = v;
+  }
+
+  // logical item -> (unit, head); workgroups of one XCD share windows (see header)
+  const int nxcd_wg = gridDim.x >> 3;           // grid is a multiple of 8
+  auto item_of = [&](int it) -> int {
+    const int b = blockIdx.x;
+    return it * gridDim.x + (b & 7) * nxcd_wg + (b >> 3);
+  };
+  struct Geo { int b, Y0, X0, head; bool edge; };
+  auto geo = [&](int item) -> Geo {
+    const int unit = item / p.heads;
+    Geo o;
+    o.head = item - unit * p.heads;
+    o.b = unit / p.upi;
+    const int wi = unit - o.b * p.upi;
+    o.Y0 = (wi / p.nwx) * S;
+    o.X0 = (wi % p.nwx) * S;
+    o.edge = o.Y0 + S > p.H || o.X0 + S > p.W;
+    return o;
+  };
+
+  // ---- per-lane DMA chunk table (item-invariant): offset of the chunk relative to the item's
+  // first token (elements) for token chunks, or into g_onehot16; kind in the top bits
+  // (0 token K/V data, 1 one-hot, 2 zero).  Edge windows re-derive (row, slot) on a slow path.
+  uint32_t chunk[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int c = (wave * NI + i) * 64 + lane;
+    const bool isv = c >= KC;
+    const int cc = isv ? c - KC : c;
+    const int per = isv ? D8 : KCH;
+    const int key = cc / per, d8 = cc - (cc / per) * per;
+    const int r = key / S, slot = key - (key / S) * S;
+    uint32_t e;
+    if (c >= KC + VC) e = 2u << 30;
+    else if (!isv && d8 >= D8) e = (1u << 30) | (uint32_t)((r < S ? r : 15) * 16 + 8 * (d8 - D8));
+    else if (r >= S) e = 2u << 30;
+    else e = (uint32_t)((r * p.W + slot) * ts + (isv ? 2 * C : C) + d8 * 8);
+    chunk[i] = e;
+  }
+  auto issue = [&](const Geo& q, int buf) {
+    const _Float16* tok0 = p.qkv + (((int64_t)q.b * p.H + q.Y0) * p.W + q.X0) * ts + q.head * D;
+    const _Float16* onehot = (const _Float16*)&g_onehot16;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      uint32_t e = chunk[i];
+      asm volatile("" : "+v"(e));   // no loop-invariant 64-bit pointers hoisted out of the item loop
+      const uint32_t kind = e >> 30, off = e & 0x3FFFFFFFu;
+      const _Float16* src = kind == 0 ? tok0 + off : (kind == 1 ? onehot + off : g_zero16);
+      if (q.edge && kind == 0) {   // pad token of an edge window: its K/V = the qkv bias
+        const int c = (wave * NI + i) * 64 + lane;
+        const bool isv = c >= KC;
+        const int cc = isv ? c - KC : c;
+        const int per = isv ? D8 : KCH;
+        const int key = cc / per, d8 = cc - (cc / per) * per;
+        const int r = key / S, slot = key - (key / S) * S;
+        if (q.Y0 + r >= p.H || q.X0 + slot >= p.W)
+          src = p.qkv_bias ? p.qkv_bias + (isv ? 2 * C : C) + q.head * D + d8 * 8 : g_zero16;
+      }
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)src,
+                                       (SAMQ_LDS void*)(bufs + buf * BUFB + (wave * NI + i) * 1024), 16, 0, 0);
+    }
+  };
+  // Q of this wave's tiles (query row wave*QT + t, slots ql) -> registers, unscaled; every lane
+  // issues every load (zero source for absent data) so the vmcnt count is wave-uniform
+  auto load_q = [&](const Geo& q, half8_t (&qv)[QT][KS]) {
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int qr = wave * QT + t;
+      const bool inwin = qr < S && ql < S;
+      const bool real = inwin && q.Y0 + qr < p.H && q.X0 + ql < p.W;
+      const int64_t tok = ((int64_t)q.b * p.H + (q.Y0 + qr)) * p.W + (q.X0 + ql);
+      const _Float16* pad = (inwin && p.qkv_bias) ? p.qkv_bias + q.head * D : nullptr;
+      const _Float16* src = real ? p.qkv + tok * ts + q.head * D : pad;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const _Float16* a = (src && (s < 2 || qin2)) ? src + 32 * s + 8 * g : g_zero16;
+        asm volatile("" : "+v"(a));   // opaque: keeps the compiler from splitting the loads by source
+        qv[t][s] = *(const SAMQ_GLOBAL half8_t*)a;
+      }
+    }
+  };
+
+  int it = 0;
+  int item = item_of(0);
+  if (item >= items) return;
+  Geo cur = geo(item);
+  half8_t qn[QT][KS];
+  issue(cur, 0);
+  load_q(cur, qn);
+
+  const int trow = ql >> 2;            // ds_read_b64_tr_b16 addressing (see rel_attention_kernel)
+  const int tcol = 4 * (ql & 3);
+  char* th_w = th16 + wave * (QT * 16 * 32);
+  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
+  int buf = 0;
+
+  for (;;) {
+    wait_vmcnt<0>();
+    __syncthreads();   // item's K/V + Q landed and visible; the other buffer is free (all waves past it)
+    half8_t qf[QT][KS];
+#pragma unroll
+    for (int t = 0; t < QT; ++t)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        half8_t v = qn[t][s];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * qscale);
+        qf[t][s] = v;
+      }
+    const int nitem = item_of(it + 1);
+    const bool has_next = nitem < items;
+    Geo nxt = cur;
+    if (has_next) {
+      nxt = geo(nitem);
+      issue(nxt, buf ^ 1);
+      load_q(nxt, qn);
+    }
+
+    // ---- rel-pos terms: TW -> C input (slots >= S masked to -inf); TH -> the Q' extra dims
+    float4_t tw[QT];
+    const float inv_scale = 1.0f / p.scale;    // (Qs . R) / scale = log2e * (q . R)
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int qr = wave * QT + t;
+      const int qh = qr < S ? qr : S - 1;
+      int r = qh - ql + S - 1;
+      r = r < 0 ? 0 : r;
+      float4_t th, tww;
+#pragma unroll
+      for (int which = 0; which < 2; ++which) {
+        const _Float16* rp = (which ? tab_w : tab_h) + r * D;
+        float4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)   // k-step 2 of lanes without q dims multiplies zeros
+          a = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const half8_t*)(rp + 32 * s + 8 * g), qf[t][s], a, 0, 0, 0);
+        a = a * inv_scale;
+        if (which) tww = a; else th = a;
+      }
+      if (g == 3) { tww[2] = -INFINITY; tww[3] = -INFINITY; }   // key slots 14, 15
+      tw[t] = tww;
+      // lane (g, ql) holds TH[kh = 4g..4g+3][ql]; lanes of groups GTH, GTH+1 need kh 0..7 / 8..15
+      *(half4_t*)(th_w + (t * 16 + ql) * 32 + 8 * g) =
+          half4_t{(_Float16)th[0], (_Float16)th[1], (_Float16)th[2], (_Float16)th[3]};
+      const half8_t thv = *(const half8_t*)(th_w + (t * 16 + ql) * 32 + 16 * (g - GTH > 0 ? 1 : 0));
+      half8_t q2 = qin2 ? qf[t][2] : half8_t{};
+      qf[t][2] = thl ? thv : q2;
+    }
+
+    const char* kb = bufs + buf * BUFB;
+    const char* vb = kb + KC * 16;
+
+    // ---- scores S^T = K'.Q'^T + TW for all key rows
+    float4_t sc[QT][S];
+#pragma unroll
+    for (int kh = 0; kh < S; ++kh) {
+      half8_t kf[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[s] = *(const half8_t*)(kb + (kh * S + ql) * KROW + (32 * s + 8 * g) * 2);
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        float4_t a = tw[t];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[t][s], a, 0, 0, 0);
+        sc[t][kh] = a;
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the K' loads of row kh next to their MFMAs
+    }
+
+    // ---- exact softmax over the window (exp2 domain)
+    half8_t pb[QT][S / 2];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      float mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
+      mx = max3f(mx, sc[t][0][3], sc[t][1][0]);
+      mx = max3f(mx, sc[t][1][1], sc[t][1][2]);
+      mx = fmaxf(mx, sc[t][1][3]);
+#pragma unroll
+      for (int kh = 2; kh < S; ++kh) {
+        mx = max3f(mx, sc[t][kh][0], sc[t][kh][1]);
+        mx = max3f(mx, sc[t][kh][2], sc[t][kh][3]);
+      }
+      mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+#pragma unroll
+      for (int pr = 0; pr < S / 2; ++pr)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pb[t][pr][r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr][r] - mx);
+          pb[t][pr][4 + r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr + 1][r] - mx);
+        }
+    }
+
+    // ---- O^T = V^T . P^T (two key rows per MFMA; V^T fragments of the next pair in flight),
+    // l = ones . P^T
+    float4_t o[QT][DT], lsum[QT];
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      lsum[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int d = 0; d < DT; ++d) o[t][d] = float4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    const uint32_t vaddr = lds_addr(vb + ((4 * g + trow) * D + tcol) * 2);
+    half4_t vlo[2][DT], vhi[2][DT];
+#pragma unroll
+    for (int d = 0; d < DT; ++d) {
+      vlo[0][d] = ds_read_tr16(vaddr + d * 32);
+      vhi[0][d] = ds_read_tr16(vaddr + S * D * 2 + d * 32);
+    }
+#pragma unroll
+    for (int pr = 0; pr < S / 2; ++pr) {
+      const int cb = pr & 1;
+      if (pr + 1 < S / 2) {
+#pragma unroll
+        for (int d = 0; d < DT; ++d) {
+          vlo[cb ^ 1][d] = ds_read_tr16(vaddr + (2 * pr + 2) * S * D * 2 + d * 32);
+          vhi[cb ^ 1][d] = ds_read_tr16(vaddr + (2 * pr + 3) * S * D * 2 + d * 32);
+        }
+      }
+      // this pair's fragments landed (the next pair's 2*DT reads may still be in flight)
+      if constexpr (DT == 5) {
+        if (pr + 1 < S / 2)
+          asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(vlo[cb][0]), "+v"(vlo[cb][1]), "+v"(vlo[cb][2]), "+v"(vlo[cb][3]),
+                       "+v"(vlo[cb][4]), "+v"(vhi[cb][0]), "+v"(vhi[cb][1]), "+v"(vhi[cb][2]), "+v"(vhi[cb][3]), "+v"(vhi[cb][4]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[cb][0]), "+v"(vlo[cb][1]), "+v"(vlo[cb][2]), "+v"(vlo[cb][3]),
+                       "+v"(vlo[cb][4]), "+v"(vhi[cb][0]), "+v"(vhi[cb][1]), "+v"(vhi[cb][2]), "+v"(vhi[cb][3]), "+v"(vhi[cb][4]));
+      } else {
+        if (pr + 1 < S / 2)
+          asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(vlo[cb][0]), "+v"(vlo[cb][1]), "+v"(vlo[cb][2]), "+v"(vlo[cb][3]),
+                       "+v"(vhi[cb][0]), "+v"(vhi[cb][1]), "+v"(vhi[cb][2]), "+v"(vhi[cb][3]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vlo[cb][0]), "+v"(vlo[cb][1]), "+v"(vlo[cb][2]), "+v"(vlo[cb][3]),
+                       "+v"(vhi[cb][0]), "+v"(vhi[cb][1]), "+v"(vhi[cb][2]), "+v"(vhi[cb][3]));
+      }
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        const half8_t va = {vlo[cb][d][0], vlo[cb][d][1], vlo[cb][d][2], vlo[cb][d][3],
+                            vhi[cb][d][0], vhi[cb][d][1], vhi[cb][d][2], vhi[cb][d][3]};
+#pragma unroll
+        for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][pr], o[t][d], 0, 0, 0);
+      }
+#pragma unroll
+      for (int t = 0; t < QT; ++t) lsum[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pb[t][pr], lsum[t], 0, 0, 0);
+    }
+
+    // ---- normalise + store (token-major [B, H, W, C])
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int qr = wave * QT + t;
+      if (qr >= S || ql >= S || cur.Y0 + qr >= p.H || cur.X0 + ql >= p.W) continue;
+      const float inv = 1.0f / lsum[t][0];
+      _Float16* dst = p.out + (((int64_t)cur.b * p.H + (cur.Y0 + qr)) * p.W + (cur.X0 + ql)) * C + cur.head * D;
+#pragma unroll
+      for (int d = 0; d < DT; ++d) {
+        half4_t v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (_Float16)(o[t][d][r] * inv);
+        *(half4_t*)(dst + d * 16 + 4 * g) = v;
+      }
+    }
+
+    if (!has_next) break;
+    ++it;
+    item = nitem;
+    cur = nxt;
+    buf ^= 1;
+  }
+}
+
+template <int D>
+static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
+  const int items = units * p.heads;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int grid = cus < items ? cus : items;
+  grid = (grid + 7) & ~7;   // multiple of 8 (XCD-aware item numbering); surplus workgroups exit
+  hipLaunchKernelGGL((win_attention_kernel<D>), dim3(grid), dim3(64 * 7), 0, stream, p, items);
+  SAMQ_LAUNCH_CHECK("win_attention launch");
+  return SAMQ_OK;
+}
+
 template <int D, int SP, int QT, int NW, bool RES, bool PRE, int RS = 16, int SC = 0>
 static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
   const int tiles = p.S * (SP / 16);
@@ -410,6 +764,8 @@ static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
 template <bool PRE>
 static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t stream) {
   const int S = p.S;
+  if (!PRE && S == 14)   // SAM's window size: persistent double-buffered kernel
+    return hd == 80 ? launch_win<80>(p, units, stream) : launch_win<64>(p, units, stream);
   if (S <= 16) {  // whole window / small grid resident in LDS; one query tile per grid row
     if (S == 14)
       return hd == 80 ? launch_attn<80, 16, 2, 7, true, PRE, 14, 14>(p, units, stream)

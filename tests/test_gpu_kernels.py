@@ -151,6 +151,8 @@ def _attn_case(b, h, w, heads, d, window, seed):
 @pytest.mark.parametrize("b,h,w,heads,d,window", [
     (2, 64, 64, 2, 80, 14),     # ViT-H windowed geometry (25 windows, pad 6)
     (1, 20, 33, 3, 64, 14),     # ragged grid, vit_b head dim
+    (4, 64, 64, 16, 80, 14),    # ViT-H B=4 windowed: 1600 (window, head) items, ~6 per persistent workgroup
+    (3, 64, 64, 12, 64, 14),    # vit_b B=3 windowed: 900 items (a ragged last round)
     (2, 64, 64, 2, 80, 0),      # ViT-H global
     (1, 32, 32, 2, 64, 0),
     (3, 16, 16, 2, 80, 0),
