@@ -27,6 +27,8 @@
 //  * XCD-aware bijective blockIdx remap: consecutive tiles (same A rows) share an L2.
 #include "common.h"
 
+#include <cstdio>
+
 // packed-weight layout produced by samq_w4_repack (and expected by samq_w4a16_gemm)
 #ifndef SAMQ_W4_LAYOUT
 #define SAMQ_W4_LAYOUT 1
@@ -293,7 +295,7 @@ void w4a16_gemm_kernel(const _Float16* __restrict__ A, int64_t lda,
 // B ds_read_b128 lane-linear.
 template <int N>
 __device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N <= 15, "vmcnt");
+  static_assert(N >= 0 && N <= 63, "vmcnt");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
@@ -700,6 +702,304 @@ void w4a16_gemm_v4(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
     }
 }
 
+// y = acc * s[n] + b[n] (-> GELU / residual add), staged through LDS in EP_ROWS-row slices per
+// wave so the global traffic is row-contiguous 16-byte vectors (v3's epilogue)
+template <int TM, int TN, int EP_ROWS, int EPI>
+__device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], const float (&csc)[TN],
+                                            const float (&cb)[TN], char* ep_bytes, void* Cout, int64_t ldc,
+                                            int M, int row_base, int col_base, int lane) {
+  constexpr int WN = TN * 32;
+  constexpr int NSL = 32 / EP_ROWS;
+  float* ep = (float*)ep_bytes;
+  const int hsel = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int sl = 0; sl < NSL; ++sl) {
+#pragma unroll
+      for (int rq = 0; rq < 16 / NSL; ++rq) {
+        const int r = sl * (16 / NSL) + rq;
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel - sl * EP_ROWS;   // row within the slice
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          float v = acc[i][t][r] * csc[t] + cb[t];
+          if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast(v);
+          ep[rl * WN + t * 32 + (lane & 31)] = v;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
+      const int srow0 = row_base + i * 32 + sl * EP_ROWS;
+      if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+        constexpr int C4 = WN / 4;
+#pragma unroll
+        for (int j = 0; j < (EP_ROWS * C4 + 63) / 64; ++j) {
+          const int idx = j * 64 + lane;
+          if (idx < EP_ROWS * C4) {
+            const int rl = idx / C4, c4 = idx % C4;
+            const int row = srow0 + rl;
+            const float4_t v = ((const float4_t*)ep)[idx];
+            if (row < M) {
+              float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
+              if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+            }
+          }
+        }
+      } else {
+        constexpr int C8 = WN / 8;
+#pragma unroll
+        for (int j = 0; j < (EP_ROWS * C8 + 63) / 64; ++j) {
+          const int idx = j * 64 + lane;
+          if (idx < EP_ROWS * C8) {
+            const int rl = idx / C8, c8 = idx % C8;
+            const int row = srow0 + rl;
+            const float4_t v0 = ((const float4_t*)ep)[2 * idx];
+            const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+            if (row < M) {
+              const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                                 (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+              *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // reads done before the next slice overwrites
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------ GEMM v6 (ping-pong, k-phases)
+// As v5, but a phase is a K-PART of the tile over ALL of the wave's output tiles: phase p
+// multiplies k16-steps [p*KPP, (p+1)*KPP) for TM x TN accumulators, so every phase reads its own
+// A fragments (balanced LDS traffic, A registers for one k-part only) and unpacks its own slice
+// of the packed B words (balanced VALU); the packed B words of the whole K tile are read in
+// phase 0.  STAGES-slot ring: K tile kt+STAGES-1 is staged during tile kt (phases 1..NPH-1).
+__device__ unsigned long long g_pp_stamps[8];   // timing experiments only (cfg 73)
+
+__host__ __device__ constexpr int pp2_pre(int p, int npw, int nph, int first) {   // pieces before phase p
+  return p <= first ? 0 : (npw * (p - first)) / (nph - first);
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_le(int n) {   // s_waitcnt vmcnt(n) for a uniform n <= N
+  if constexpr (N > 0) {
+    if (n >= N) { vm_wait<N>(); return; }
+    vm_wait_le<N - 1>(n);
+  } else {
+    vm_wait<0>();
+  }
+}
+
+template <int WAVES_M, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
+__global__ __launch_bounds__(512, 1)
+void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
+                    const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
+                    const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
+                    int M, int N, int K) {
+  constexpr int NW = 8;
+  constexpr int WAVES_N = NW / WAVES_M;
+  constexpr int WM = TM * 32, WN = TN * 32;
+  constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
+  constexpr int BK = 64, ROWB = BK * 2;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB;
+  constexpr int NPW = (NT + NW - 1) / NW;
+  constexpr int STAGE = A_BYTES + NB * 1024;
+  constexpr int KPP = 4 / NPH;
+  // K tile kt+LA is staged during tile kt (slot of tile kt+LA-STAGES, last read during tile kt-1
+  // at the latest), its pieces issued behind the MFMA bursts: a wave's MFMA half of phase 0
+  // starts after the barrier that ends every read of tile kt-1 (both groups' load halves of
+  // tile kt-1's last phase lie before it, and their lgkmcnt waits precede their MFMAs), so all
+  // phases may restage (WAR).  The retire wait for tile kt+1 sits in the load half of the last
+  // phase, before the barrier after which the first group reads it (RAW).
+  constexpr int PRE_LAST = pp2_pre(NPH - 1, NPW, NPH, 0);
+  constexpr int EP_ROWS = WN > 64 ? 16 : 32;
+  constexpr int EP_BYTES = EP_ROWS * WN * 4;
+  constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
+  static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
+  static_assert(LA >= 2 && LA < STAGES, "ring");
+  static_assert((LA - 2) * NPW + PRE_LAST <= 63, "vmcnt");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+  const int grp = wave >> 2;
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = K / BK;
+
+  const char* src[NPW];
+  int dst[NPW];
+  int step[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    int j = wave * NPW + i;
+    j = j < NT ? j : NT - 1;
+    if (j < NA) {
+      const int row = j * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      src[i] = (const char*)(A + (int64_t)gr * lda + c * 8);
+      dst[i] = j * 1024;
+      step[i] = BK * 2;
+    } else {
+      const int nt = n0 / 32 + (j - NA);
+      src[i] = (const char*)(Wp + ((int64_t)nt * kt_count) * 64 + lane);
+      dst[i] = A_BYTES + (j - NA) * 1024;
+      step[i] = 64 * 16;
+    }
+  }
+  auto issue = [&](int kt, int slot, int i0, int i1) {
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+      if (i >= i0 && i < i1)
+        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)kt * step[i]),
+                                         (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+  };
+
+  int col[TN];
+  half2_t zc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+    const uint32_t zw = qzeros[col[t] >> 3];
+    const _Float16 z = (_Float16)(1024 + (int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
+    zc[t] = half2_t{z, z};
+  }
+  uint32_t kMask = 0x000F000Fu, kMagic = 0x64006400u;
+  asm volatile("" : "+v"(kMask), "+v"(kMagic));
+
+  float16_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int hsel = lane >> 5;
+  int a_off[TM], a_swz[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_off[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
+  }
+
+  // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
+  const int pro = kt_count < LA ? kt_count : LA;
+#pragma unroll
+  for (int j = 0; j < LA; ++j)
+    if (j < pro) issue(j, j, 0, NPW);
+  vm_wait_le<(LA - 1) * NPW>((pro - 1) * NPW);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // VAR & 4 (timing experiment): per-wave cycles of the load half, barrier 1, MFMA half, barrier 2
+  unsigned long long ph[4] = {0, 0, 0, 0}, tprev = 0;
+  auto stamp = [&](int k) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (tprev) ph[k] += t - tprev;
+    tprev = t;
+  };
+  int slot = 0;
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const char* st = smem + slot * STAGE;
+    const int ahead = kt + LA;
+    const bool pf = ahead < kt_count && !(VAR & 1);   // VAR & 1: timing-only, no restaging
+    const int sa = slot + LA >= STAGES ? slot + LA - STAGES : slot + LA;   // (kt + LA) % STAGES
+    u32x4 bw[TN];
+#pragma unroll
+    for (int p = 0; p < NPH; ++p) {
+      // ---------------- load half
+      if (p == NPH - 1 && kt + 1 < kt_count) {
+        // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
+        int newer = pf ? PRE_LAST : 0;
+#pragma unroll
+        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
+        vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+      }
+      if (p == 0) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t) bw[t] = *(const u32x4*)(st + A_BYTES + (wn * TN + t) * 1024 + lane * 16);
+      }
+      half8_t af[TM][KPP];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int s = 0; s < KPP; ++s)
+          af[i][s] = *(const half8_t*)(st + a_off[i] + (((2 * (p * KPP + s) + hsel) ^ a_swz[i]) << 4));
+      half8_t bf[TN][KPP];
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int s = 0; s < KPP; ++s) {
+          const uint32_t w = bw[t][p * KPP + s];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const half2_t h = __builtin_bit_cast(half2_t, ((w >> (4 * i)) & kMask) | kMagic) - zc[t];
+            bf[t][s][2 * i] = h[0];
+            bf[t][s][2 * i + 1] = h[1];
+          }
+        }
+      if (VAR & 4) stamp(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (VAR & 4) stamp(1);
+      // ---------------- MFMA half
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < KPP; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int t = 0; t < TN; ++t) {
+            if (VAR & 2) {   // timing-only: no MFMA
+              acc[i][t][0] += (float)af[i][s][0] * (float)bf[t][s][1];
+            } else {
+              acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+            }
+          }
+      // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
+      // the barrier otherwise; WAR-safe in every phase: see header)
+      if (pf) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
+      if (VAR & 4) stamp(2);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (VAR & 4) stamp(3);
+    }
+    slot = slot == STAGES - 1 ? 0 : slot + 1;
+  }
+  if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
+  if ((VAR & 4) && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_pp_stamps[k], ph[k]);
+    atomicAdd(&g_pp_stamps[4], (unsigned long long)kt_count * NPH);
+  }
+
+  float csc[TN], cb[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    csc[t] = (float)scales[col[t]];
+    cb[t] = bias ? (float)bias[col[t]] : 0.0f;
+  }
+  __syncthreads();
+  pp_epilogue<TM, TN, EP_ROWS, EPI>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
+                                    n0 + wn * WN, lane);
+}
+
 // ------------------------------------------------------------------ dispatch
 struct GemmArgs {
   const _Float16* A; int64_t lda; const u32x4* Wp; const _Float16* scales; const uint32_t* qzeros;
@@ -733,8 +1033,44 @@ static int launch_v4(const GemmArgs& a, hipStream_t st) {
   return SAMQ_OK;
 }
 
+template <int WMW, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
+static int launch_pp2(const GemmArgs& a, hipStream_t st) {
+  constexpr int BM = WMW * TM * 32, BN = (8 / WMW) * TN * 32;
+  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
+                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K);
+  SAMQ_LAUNCH_CHECK("w4a16_gemm_pp2 launch");
+  return SAMQ_OK;
+}
+
 template <int EPI, bool GR>
 static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
+  if (cfg >= 50 && cfg < 80) {   // ping-pong kernels: per-channel scales only (groupsize == K)
+    if (GR) return fail(SAMQ_ERR_INVALID, "w4a16_gemm: ping-pong configs need groupsize == K");
+    switch (cfg) {
+      case 55: return launch_pp2<2, 4, 2, 2, 3, 2, EPI>(a, st);   // v6 256x256, 2 k-phases, 3 slots
+      case 56: return launch_pp2<2, 4, 2, 2, 4, 2, EPI>(a, st);   // 4 slots, lookahead 2 (DMA in both phases)
+      case 57: return launch_pp2<2, 4, 2, 2, 4, 3, EPI>(a, st);   // 4 slots, lookahead 3
+      case 58: return launch_pp2<2, 4, 2, 1, 4, 2, EPI>(a, st);   // 1 phase / K tile, 4 slots, lookahead 2
+      case 60: return launch_pp2<1, 8, 1, 2, 4, 3, EPI>(a, st);   // 1x8 waves (256x32 each): B unpacked once
+      case 61: return launch_pp2<1, 8, 1, 4, 4, 3, EPI>(a, st);   // 1x8 waves, 4 k-phases
+      case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
+      case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
+      case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
+      case 73: {   // timing experiment: cfg 57 with per-segment s_memtime stamps (synchronous)
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0}, h[8];
+        hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), z, sizeof(z));
+        const int r = launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4>(a, st);
+        hipStreamSynchronize(st);
+        hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pp_stamps), sizeof(h));
+        const double n = (double)h[4];
+        fprintf(stderr, "pp2 stamps (cycles per wave-phase): load %.0f  barrier1 %.0f  mfma %.0f  barrier2 %.0f\n",
+                h[0] / n, h[1] / n, h[2] / n, h[3] / n);
+        return r;
+      }
+      default: break;
+    }
+  }
   switch (cfg) {
     case 21: return launch_v3<256, 256, 2, 4, EPI, GR>(a, st);
     case 22: return launch_v3<128, 256, 2, 4, EPI, GR>(a, st);
@@ -771,7 +1107,11 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
 // Measured on MI355X (tools/bench_gemm.py, ViT-H shapes at M = 16384): the 3-stage LDS-DMA
 // kernel with 128x256 tiles / 64x64 wave tiles (cfg 22, 2 workgroups per CU) is the fastest or
 // within 2 % of it on every projection shape and beats dense fp16 hipBLASLt on 3 of 4.
-static int pick_cfg(int M, int N) {
+// The ping-pong v6 (cfg 57: 256x256 tiles, 4-slot ring, lookahead 3) is 5-7 % faster on the wide
+// projections (qkv N=3840, lin1 N=5120 at M=16384: 1090 / 970 TF/s vs 1016 / 925); with N=1280 its
+// 320 tiles leave a 25 % second round on 256 CUs, where v3's 2-workgroup/CU 128x256 stays ahead.
+static int pick_cfg(int M, int N, bool grouped) {
+  if (!grouped && N % 256 == 0 && N >= 2048 && M >= 4096) return 57;
   if (N % 256 == 0 && M >= 1024) return 22;
   if (N % 128 == 0 && M >= 512) return 23;
   if (N % 64 == 0) return 26;
@@ -786,6 +1126,9 @@ static int cfg_bn(int cfg) {
                  case 27: return 256; case 28: return 256; case 29: return 320; case 30: return 320;
                  case 31: return 320; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
+                 case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
+                 case 60: return 256; case 61: return 256;
+                 case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }
 }
 
@@ -838,11 +1181,11 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
   // the v3 kernels (cfg 21-28) store 16-byte row vectors: C 16-byte aligned, ldc % 8 == 0
   const bool vec_ok = ((uintptr_t)C & 15) == 0 && ldc % 8 == 0;
   if (cfg <= 0) {
-    cfg = pick_cfg(M, N);
-    if (!vec_ok && cfg >= 21 && cfg <= 31) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
+    cfg = pick_cfg(M, N, groupsize != -1 && groupsize != K);
+    if (!vec_ok && ((cfg >= 21 && cfg <= 31) || cfg >= 50)) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
   }
   SAMQ_REQUIRE(cfg_bn(cfg) > 0 && N % cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a16_gemm: N not divisible by tile");
-  SAMQ_REQUIRE(vec_ok || cfg < 21 || cfg > 31, SAMQ_ERR_INVALID,
+  SAMQ_REQUIRE(vec_ok || ((cfg < 21 || cfg > 31) && cfg < 50), SAMQ_ERR_INVALID,
                "w4a16_gemm: this tile config needs a 16-byte aligned C with ldc % 8 == 0");
   GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
              (const _Float16*)bias, C, ldc, M, N, K, groupsize};

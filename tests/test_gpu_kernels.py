@@ -82,6 +82,51 @@ def test_w4a16_gemm_epilogues(cuda, epi):
         _close(out, y, 2e-5)
 
 
+def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rng):
+    args = (_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, groupsize)
+    tol = 2e-3 if groupsize == -1 else 4e-3
+    if epi == "bias":
+        _close(ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=cfg), y, tol)
+    elif epi == "gelu":
+        _close(ops.w4a16_gemm(*args, ops.EPI_BIAS_GELU, cfg=cfg), sam_ref.gelu_erf(torch.from_numpy(y)).numpy(), tol)
+    elif epi == "resadd":
+        r0 = rng.standard_normal(y.shape, dtype=np.float32)
+        res = _dev(r0, cuda)
+        ops.w4a16_gemm(*args, ops.EPI_RESADD_F32, out=res, cfg=cfg)
+        _close(res, r0 + y, 2e-5 if groupsize == -1 else 4e-3)
+    else:
+        _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
+
+
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
+def test_w4a16_gemm_pingpong(cuda, cfg, epi):
+    """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
+    ragged M, short and long K (1 .. 40 K tiles, so the ring prologue / retire paths all run)."""
+    from samq import ops
+    for m, k, n in ((333, 1280, 512), (300, 64, 256), (260, 192, 256), (513, 2560, 768)):
+        qw, qz, sc, bias = _packed_layer(k, n, -1, seed=cfg * 13 + k)
+        rng = np.random.Generator(np.random.PCG64(cfg + k))
+        a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+        y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
+        _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, -1, epi, cfg, rng)
+
+
+@pytest.mark.parametrize("groupsize", [-1, 128])
+def test_w4a16_gemm_auto_pick_wide(cuda, groupsize):
+    """The automatic tile choice at the ViT-H wide shapes (M >= 4096, N >= 2048: ping-pong v6 for
+    per-channel weights, v3 for grouped ones) against the oracle."""
+    from samq import ops
+    m, k, n = 4133, 1280, 2304
+    qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=77 + (groupsize > 0))
+    rng = np.random.Generator(np.random.PCG64(78))
+    a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+    y = gptq_pack.matmul4_g1(a, qw, sc, qz, groupsize, bias)
+    packed = ops.w4_repack(_dev(qw, cuda))
+    for epi in ("bias", "gelu", "resadd"):
+        _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, 0, rng)
+
+
 @pytest.mark.parametrize("tag", ["gm1", "g128"])
 def test_matmul4_functional_vs_reference_golden(cuda, golden_dir, tag):
     """``triton_matmul4`` drop-in on the reference's own fixture: within fp16 rounding of the

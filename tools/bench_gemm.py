@@ -45,7 +45,7 @@ def main():
         pack_linear(q, fake, s, z, torch.randn(n, device=dev) * 0.02)
         packed = q.prepare()
         packed2 = ops.w4_repack(q.qweight, layout=2)
-        pk = lambda c: packed2 if c >= 40 else packed  # noqa: E731
+        pk = lambda c: packed2 if 40 <= c < 50 else packed  # noqa: E731
         a = torch.randn(m, k, device=dev).half()
         f32 = epi in (ops.EPI_RESADD_F32, ops.EPI_F32)
         outs = {}
