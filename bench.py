@@ -87,12 +87,13 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
     for p in eng.plans:
         for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
             alg.append(rows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + rows * lin.outfeatures * out_b)
-    traffic, src = pmc_traffic("w4a16_gemm_v3", "r1_pmc_traffic_w4a16.json") if bufs_batch == 4 else (None, None)
+    traffic, src = pmc_traffic("w4a16_gemm", "r1_pmc_traffic_w4a16.json") if bufs_batch == 4 else (None, None)
     return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_FP16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_FP16_TFLOPS, 4), traffic=traffic,
                 traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
                 algorithmic_bytes_per_launch=round(sum(alg) / len(alg)),
-                kernel="w4a16_gemm_v3 (all 4 ViT-H projection shapes)", launches_timed=n,
+                kernel="w4a16_gemm_pp2 (qkv, lin1) + w4a16_gemm_v3 (proj, lin2): all 4 ViT-H projection shapes",
+                launches_timed=n,
                 avg_launch_us=round(t / n * 1e6, 2))
 
 
