@@ -198,6 +198,28 @@ int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float*
                           int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
                           float s_out, hipStream_t stream);
 
+/* ---------------------------------------------------------------- patch embedding / neck */
+
+/* PatchEmbed (segment_anything/modeling/image_encoder.py:411-442) + pos_embed add (:108-110)
+ * as one implicit GEMM: img f16 [B, Cin, S, S] (NCHW, S = img_size), weight f16 [N, Cin*p*p]
+ * (the Conv2d weight flattened (c, kh, kw)), bias f32 [N] or NULL, pos f32 [(S/p)^2, N] or NULL
+ * -> out f32 [B, S/p, S/p, N] (the residual stream; fp32 accumulate, no fp16 rounding).
+ * patch % 8 == 0, Cin*p*p % 32 == 0, N % 128 == 0. */
+int samq_patch_embed(const void* img, const void* weight, const float* bias, const float* pos, float* out,
+                     int B, int Cin, int img_size, int patch, int N, hipStream_t stream);
+
+/* Neck 1x1 conv, no bias (image_encoder.py:88-104 neck[0]) on the fp32 token rows:
+ * x f32 [M, K] (converted to f16 on load, as the reference's fp16 neck), weight f16 [N, K]
+ * -> out f16 [M, N].  K % 32 == 0, N % 128 == 0. */
+int samq_conv1x1_f32(const float* x, const void* weight, void* out, int64_t M, int N, int K,
+                     hipStream_t stream);
+
+/* Neck 3x3 conv, padding 1, no bias (neck[2]) on an NHWC f16 map: x f16 [B, G, G, Cin],
+ * weight f16 [N, 3, 3, Cin] (the Conv2d weight permuted (n, ky, kx, c)) -> out f16 [B, G, G, N].
+ * Cin % 32 == 0, N % 128 == 0. */
+int samq_conv3x3_nhwc(const void* x, const void* weight, void* out, int B, int G, int Cin, int N,
+                      hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

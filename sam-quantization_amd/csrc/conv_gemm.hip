@@ -1,0 +1,207 @@
+// Implicit-GEMM convolutions of the encoder's patch embedding and neck on fp16 MFMA.
+//
+// Replaces the last vendor-BLAS / im2col pieces of the encoder forward:
+//  * PatchEmbed: Conv2d(3, C, 16, stride 16) + pos_embed add (segment_anything/modeling/
+//    image_encoder.py:411-442, :108-110): the 16x16 patches are gathered straight from the NCHW
+//    image into the A operand (no im2col copy), bias and the absolute position embedding are
+//    added in the fp32 epilogue, the fp32 residual stream is written directly;
+//  * neck conv 1x1 (C -> 256, no bias, image_encoder.py:88-104): A = the fp32 residual tokens,
+//    converted to fp16 while staged (the reference runs the neck in fp16);
+//  * neck conv 3x3 pad 1 (256 -> 256, no bias): A gathered from the NHWC fp16 feature map with
+//    zero padding; the weight is pre-permuted to (n, ky, kx, c) so a 64-byte A chunk is 32
+//    contiguous channels of one tap.
+// Small GEMMs (0.3 % of the encoder FLOPs): a plain 128x128x32 LDS double-buffered tile on
+// v_mfma_f32_32x32x16_f16, 4 waves of 64x64, fp32 accumulation.
+#include "common.h"
+
+namespace samq {
+
+enum { CG_PATCH = 0, CG_1X1_F32 = 1, CG_3X3 = 2 };
+
+struct ConvArgs {
+  const void* x;        // PATCH: image f16 [B][Cin][G*P][G*P]; 1X1_F32: f32 [M][K]; 3X3: f16 [B][G][G][Cin]
+  const _Float16* w;    // f16 [N][K]  (3X3: K ordered (ky, kx, c))
+  const float* bias;    // PATCH: f32 [N] or null
+  const float* pos;     // PATCH: f32 [G*G][N] or null
+  void* out;            // PATCH: f32 [M][N]; else f16 [M][N]
+  int M, N, K;
+  int G, P, Cin;
+};
+
+template <int MODE>
+__device__ __forceinline__ half8_t conv_load_a(const ConvArgs& a, int t, int k) {
+  // t: token index (< M), k: first of 8 consecutive reduction indices
+  const int gg = a.G * a.G;
+  const int b = t / gg, gy = (t / a.G) % a.G, gx = t % a.G;
+  if (MODE == CG_PATCH) {
+    const int pp = a.P * a.P;
+    const int c = k / pp, rem = k - c * pp, kh = rem / a.P, kw = rem - kh * a.P;
+    const int side = a.G * a.P;
+    const _Float16* src = (const _Float16*)a.x + (((int64_t)b * a.Cin + c) * side + gy * a.P + kh) * side +
+                          gx * a.P + kw;
+    return *(const half8_t*)src;
+  } else if (MODE == CG_1X1_F32) {
+    const float4_t* src = (const float4_t*)((const float*)a.x + (int64_t)t * a.K + k);
+    const float4_t v0 = src[0], v1 = src[1];
+    return half8_t{(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                   (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+  } else {
+    const int tap = k / a.Cin, c0 = k - tap * a.Cin;
+    const int sy = gy + tap / 3 - 1, sx = gx + tap % 3 - 1;
+    if (sy < 0 || sy >= a.G || sx < 0 || sx >= a.G) return half8_t{};
+    return *(const half8_t*)((const _Float16*)a.x + (((int64_t)b * a.G + sy) * a.G + sx) * a.Cin + c0);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 32;
+  constexpr int PITCH = BK * 2 + 16;   // 80-byte LDS rows: the 32 row reads of a fragment spread over banks
+  constexpr int BUF = (BM + BN) * PITCH;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = a.K / BK;
+
+  // staging: chunk c = tid + 256 j (j = 0, 1) -> row c / 4, 8 k-values at (c % 4) * 8
+  half8_t ra[2], rb[2];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, k = kt * BK + (c & 3) * 8;
+      int t = m0 + row;
+      t = t < a.M ? t : a.M - 1;
+      ra[j] = conv_load_a<MODE>(a, t, k);
+      rb[j] = *(const half8_t*)(a.w + (int64_t)(n0 + row) * a.K + k);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, off = (c & 3) * 16;
+      *(half8_t*)(smem + buf * BUF + row * PITCH + off) = ra[j];
+      *(half8_t*)(smem + buf * BUF + (BM + row) * PITCH + off) = rb[j];
+    }
+  };
+
+  float16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
+
+  const int hsel = lane >> 5;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < kt_count) load(kt + 1);
+    const char* base = smem + buf * BUF;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      half8_t af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *(const half8_t*)(base + (wm * 64 + i * 32 + (lane & 31)) * PITCH + (s * 16 + 8 * hsel) * 2);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        bf[t] = *(const half8_t*)(base + (BM + wn * 64 + t * 32 + (lane & 31)) * PITCH + (s * 16 + 8 * hsel) * 2);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[t], acc[i][t], 0, 0, 0);
+    }
+    if (kt + 1 < kt_count) {
+      store(buf ^ 1);   // the other buffer was last read before the previous barrier
+      __syncthreads();
+    }
+  }
+
+  // epilogue: lane owns column (lane & 31) of each 32x32 tile, 16 rows
+  const int gg = a.G * a.G;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = n0 + wn * 64 + t * 32 + (lane & 31);
+    const float bcol = (MODE == CG_PATCH && a.bias) ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        if (row >= a.M) continue;
+        float v = acc[i][t][r];
+        if (MODE == CG_PATCH) {
+          v += bcol;
+          if (a.pos) v += a.pos[(int64_t)(row % gg) * a.N + col];
+          ((float*)a.out)[(int64_t)row * a.N + col] = v;
+        } else {
+          ((_Float16*)a.out)[(int64_t)row * a.N + col] = (_Float16)v;
+        }
+      }
+    }
+  }
+}
+
+template <int MODE>
+static int conv_launch(const ConvArgs& a, hipStream_t stream) {
+  const int nwg = ((a.M + 127) / 128) * (a.N / 128);
+  hipLaunchKernelGGL((conv_gemm_kernel<MODE>), dim3(nwg), dim3(256), 0, stream, a);
+  SAMQ_LAUNCH_CHECK("conv_gemm launch");
+  return SAMQ_OK;
+}
+
+}  // namespace samq
+
+using namespace samq;
+
+extern "C" int samq_patch_embed(const void* img, const void* weight, const float* bias, const float* pos, float* out,
+                                int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  SAMQ_REQUIRE(img && weight && out, SAMQ_ERR_INVALID, "patch_embed: null pointer");
+  SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
+               "patch_embed: image size must be a multiple of the patch size");
+  SAMQ_REQUIRE(patch % 8 == 0 && (Cin * patch * patch) % 32 == 0, SAMQ_ERR_UNSUPPORTED,
+               "patch_embed: patch must be a multiple of 8 and Cin*patch^2 a multiple of 32");
+  SAMQ_REQUIRE(N % 128 == 0, SAMQ_ERR_UNSUPPORTED, "patch_embed: embed dim must be a multiple of 128");
+  SAMQ_REQUIRE(((uintptr_t)img & 15) == 0 && ((uintptr_t)weight & 15) == 0, SAMQ_ERR_INVALID,
+               "patch_embed: image and weight must be 16-byte aligned");
+  const int g = img_size / patch;
+  ConvArgs a{img, (const _Float16*)weight, bias, pos, out, B * g * g, N, Cin * patch * patch, g, patch, Cin};
+  return conv_launch<CG_PATCH>(a, stream);
+}
+
+extern "C" int samq_conv1x1_f32(const float* x, const void* weight, void* out, int64_t M, int N, int K,
+                                hipStream_t stream) {
+  SAMQ_REQUIRE(x && weight && out, SAMQ_ERR_INVALID, "conv1x1: null pointer");
+  SAMQ_REQUIRE(M > 0 && M < (int64_t)1 << 31, SAMQ_ERR_INVALID, "conv1x1: bad M");
+  SAMQ_REQUIRE(K % 32 == 0 && N % 128 == 0, SAMQ_ERR_UNSUPPORTED,
+               "conv1x1: K must be a multiple of 32 and N of 128");
+  SAMQ_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0, SAMQ_ERR_INVALID,
+               "conv1x1: operands must be 16-byte aligned");
+  ConvArgs a{x, (const _Float16*)weight, nullptr, nullptr, out, (int)M, N, K, 1, 1, K};
+  return conv_launch<CG_1X1_F32>(a, stream);
+}
+
+extern "C" int samq_conv3x3_nhwc(const void* x, const void* weight, void* out, int B, int G, int Cin, int N,
+                                 hipStream_t stream) {
+  SAMQ_REQUIRE(x && weight && out, SAMQ_ERR_INVALID, "conv3x3: null pointer");
+  SAMQ_REQUIRE(B > 0 && G > 0, SAMQ_ERR_INVALID, "conv3x3: bad shape");
+  SAMQ_REQUIRE(Cin % 32 == 0 && N % 128 == 0, SAMQ_ERR_UNSUPPORTED,
+               "conv3x3: Cin must be a multiple of 32 and N of 128");
+  SAMQ_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)weight & 15) == 0, SAMQ_ERR_INVALID,
+               "conv3x3: operands must be 16-byte aligned");
+  ConvArgs a{x, (const _Float16*)weight, nullptr, nullptr, out, B * G * G, N, 9 * Cin, G, 1, Cin};
+  return conv_launch<CG_3X3>(a, stream);
+}

@@ -1059,10 +1059,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
       case 73: {   // timing experiment: cfg 57 with per-segment s_memtime stamps (synchronous)
         unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0}, h[8];
-        hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), z, sizeof(z));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), z, sizeof(z));
         const int r = launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4>(a, st);
-        hipStreamSynchronize(st);
-        hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pp_stamps), sizeof(h));
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pp_stamps), sizeof(h));
         const double n = (double)h[4];
         fprintf(stderr, "pp2 stamps (cycles per wave-phase): load %.0f  barrier1 %.0f  mfma %.0f  barrier2 %.0f\n",
                 h[0] / n, h[1] / n, h[2] / n, h[3] / n);

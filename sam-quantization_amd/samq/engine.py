@@ -14,8 +14,11 @@ partition/permute/pad copies per block, fp16 residual) by 7 launches per block:
     x  += h . W2 + b2                 samq_w4a16_gemm     EPI_RESADD_F32
 
 The residual stream ``x`` stays fp32 in HBM (precision: SURVEY.md §7 "Hard parts").
-Patch embedding and the neck (0.3 % of the FLOPs) run as im2col + hipBLASLt GEMMs via torch
-on the GPU plus the HIP LayerNorm; they are the next rows to move into HIP.
+Patch embedding (+bias +pos_embed) and the neck convolutions are implicit-GEMM HIP kernels
+(``csrc/conv_gemm.hip``: patches gathered from the NCHW image, 3x3 taps from the NHWC map, no
+im2col copies) plus the HIP LayerNorm; the only torch op left is the final NHWC -> NCHW view
+change of the output.  W4A8 keeps its patch embedding in fp32 (a vendor fp32 GEMM): its first
+int8 quantiser sits right behind it.
 All activation buffers are allocated once per batch size and reused; ``capture()`` records the
 whole forward into a HIP graph for launch-overhead-free replay.
 """
@@ -77,12 +80,14 @@ class EncoderEngine:
         pe = enc.patch_embed.proj
         self.patch = pe.kernel_size[0]
         self.pe_w = pe.weight.detach().reshape(pe.weight.shape[0], -1).to(torch.float16).contiguous()
-        self.pe_b = pe.bias.detach().float() if pe.bias is not None else None
-        self.pos = enc.pos_embed.detach().float() if enc.pos_embed is not None else None
+        self.pe_b = pe.bias.detach().float().contiguous() if pe.bias is not None else None
+        self.pos = enc.pos_embed.detach().float().contiguous() if enc.pos_embed is not None else None
         n0, n1, n2, n3 = enc.neck
         self.n0_w = n0.weight.detach().reshape(n0.weight.shape[0], -1).to(torch.float16).contiguous()
         self.n1 = (n1.weight.detach().float().contiguous(), n1.bias.detach().float().contiguous(), float(n1.eps))
         self.n2_w = n2.weight.detach().reshape(n2.weight.shape[0], -1).to(torch.float16).contiguous()
+        # 3x3 taps major, channels minor: a 16-byte A chunk of the implicit GEMM is 8 channels of one tap
+        self.n2_w_tap = n2.weight.detach().permute(0, 2, 3, 1).to(torch.float16).contiguous()
         self.n3 = (n3.weight.detach().float().contiguous(), n3.bias.detach().float().contiguous(), float(n3.eps))
         self.out_chans = n0.weight.shape[0]
         self._bufs = {}
@@ -134,11 +139,16 @@ class EncoderEngine:
 
     # ---------------------------------------------------------------- stages
     def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
-        """Patch embedding as im2col + GEMM, one GEMM per image so that an image's result does
-        not depend on the batch it is in (the vendor GEMM picks its algorithm by M).  W4A8 computes
-        it in fp32: its first int8 quantiser sits right behind it."""
+        """Patch embedding + bias + pos_embed into the fp32 residual stream: one implicit-GEMM HIP
+        kernel (patches read straight from the NCHW image).  W4A8 computes it in fp32 (vendor GEMM,
+        one per image so an image's result does not depend on its batch): its first int8
+        quantiser sits right behind it."""
         b = img.shape[0]
         p, g = self.patch, self.grid
+        if not self.w4a8:
+            ops.patch_embed(img.to(torch.float16).contiguous(), self.pe_w, self.pe_b,
+                            None if self.pos is None else self.pos[0], p, out=x32)
+            return
         dt = torch.float32 if self.w4a8 else torch.float16
         w = self.pe_w.to(dt) if self.w4a8 else self.pe_w
         cols = img.to(dt).reshape(b, -1, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(b, g * g, -1)
@@ -176,15 +186,13 @@ class EncoderEngine:
         p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
 
     def neck(self, x32: torch.Tensor, out_dtype) -> torch.Tensor:
+        """Neck (image_encoder.py:88-104) on NHWC tokens: 1x1 conv (HIP, fp32 tokens -> fp16),
+        LayerNorm2d (HIP), 3x3 conv (HIP implicit GEMM, zero padding in the gather), LayerNorm2d."""
         b, g = x32.shape[0], self.grid
-        oc = self.out_chans
-        x16 = x32.view(b, -1, self.C).to(torch.float16)
-        y = torch.stack([torch.matmul(x16[i], self.n0_w.t()) for i in range(b)])          # 1x1 conv (per image)
-        y = ops.layernorm(y.view(b, g, g, oc), *self.n1[:2], eps=self.n1[2])                # LN2d (NHWC rows)
-        cols = F.unfold(y.permute(0, 3, 1, 2), kernel_size=3, padding=1)                    # (b, oc*9, g*g)
-        y = torch.stack([torch.matmul(cols[i].t(), self.n2_w.t()) for i in range(b)])       # 3x3 conv
-        y = ops.layernorm(y.reshape(b, g, g, oc).contiguous(), *self.n3[:2], eps=self.n3[2],
-                          out_dtype=torch.float32)
+        y = ops.conv1x1_f32(x32, self.n0_w)                                                # (b, g, g, oc) f16
+        y = ops.layernorm(y, *self.n1[:2], eps=self.n1[2])                                 # LN2d (NHWC rows)
+        y = ops.conv3x3_nhwc(y, self.n2_w_tap)                                             # 3x3, pad 1
+        y = ops.layernorm(y, *self.n3[:2], eps=self.n3[2], out_dtype=torch.float32)
         return y.permute(0, 3, 1, 2).to(out_dtype)
 
     # ---------------------------------------------------------------- forward

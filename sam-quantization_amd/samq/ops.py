@@ -96,6 +96,56 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     return out
 
 
+# ----------------------------------------------------------------------------- patch embed / neck
+def patch_embed(img: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], pos: Optional[torch.Tensor],
+                patch: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """img f16 (B, Cin, S, S) -> f32 (B, S/p, S/p, N) = Conv2d(k=p, stride=p)(img) + bias + pos;
+    weight f16 (N, Cin*p*p), bias f32 (N,), pos f32 (S/p, S/p, N) or None."""
+    _need_cuda(img, weight, bias, pos)
+    b, cin, s, s2 = img.shape
+    assert s == s2 and img.dtype == torch.float16 and img.is_contiguous()
+    n = weight.shape[0]
+    assert weight.dtype == torch.float16 and weight.is_contiguous() and weight.shape[1] == cin * patch * patch
+    assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
+    assert pos is None or (pos.dtype == torch.float32 and pos.is_contiguous() and pos.numel() == (s // patch) ** 2 * n)
+    g = s // patch
+    if out is None:
+        out = torch.empty((b, g, g, n), dtype=torch.float32, device=img.device)
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == b * g * g * n
+    _lib.check(_lib.load().samq_patch_embed(_ptr(img), _ptr(weight), _ptr(bias), _ptr(pos), _ptr(out), b, cin, s,
+                                            patch, n, _stream()), "patch_embed")
+    return out
+
+
+def conv1x1_f32(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x f32 (..., K) tokens -> f16 (..., N) = x . weight^T (1x1 conv, no bias); weight f16 (N, K)."""
+    _need_cuda(x, weight)
+    k = x.shape[-1]
+    n = weight.shape[0]
+    assert x.dtype == torch.float32 and x.is_contiguous() and weight.dtype == torch.float16 and weight.shape[1] == k
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (n,), dtype=torch.float16, device=x.device)
+    assert out.dtype == torch.float16 and out.is_contiguous()
+    _lib.check(_lib.load().samq_conv1x1_f32(_ptr(x), _ptr(weight.contiguous()), _ptr(out), x.numel() // k, n, k,
+                                            _stream()), "conv1x1")
+    return out
+
+
+def conv3x3_nhwc(x: torch.Tensor, weight_tap_major: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x f16 (B, G, G, Cin) -> f16 (B, G, G, N): 3x3 conv, padding 1, no bias; weight f16 (N, 3, 3, Cin)."""
+    _need_cuda(x, weight_tap_major)
+    b, g, g2, cin = x.shape
+    assert g == g2 and x.dtype == torch.float16 and x.is_contiguous()
+    w = weight_tap_major
+    n = w.shape[0]
+    assert w.dtype == torch.float16 and w.is_contiguous() and tuple(w.shape[1:]) == (3, 3, cin)
+    if out is None:
+        out = torch.empty((b, g, g, n), dtype=torch.float16, device=x.device)
+    assert out.dtype == torch.float16 and out.is_contiguous()
+    _lib.check(_lib.load().samq_conv3x3_nhwc(_ptr(x), _ptr(w), _ptr(out), b, g, cin, n, _stream()), "conv3x3")
+    return out
+
+
 # ----------------------------------------------------------------------------- attention
 def rel_attention(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,
                   rel_pos_w: torch.Tensor, heads: int, window: int, sm_scale: float,

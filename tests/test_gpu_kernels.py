@@ -238,3 +238,46 @@ def test_attention_functional_and_module_vs_reference_golden(cuda, golden_dir, t
     with torch.no_grad():
         y = qa(_dev(f["x"], cuda))
     _close(y, f["out"].astype(np.float32), 4e-3)
+
+
+# ----------------------------------------------------------------------------- patch embed / neck (§8f f4)
+def test_patch_embed_vs_conv(cuda):
+    """Implicit-GEMM PatchEmbed (+bias +pos_embed) vs torch Conv2d in fp32 on the same fp16 values
+    (fp32 accumulation: only the summation order differs)."""
+    from samq import ops
+    g = torch.Generator().manual_seed(5)
+    b, c, p, s = 2, 768, 16, 256
+    img = torch.randn(b, 3, s, s, generator=g).half()
+    w = (torch.randn(c, 3, p, p, generator=g) * 0.02).half()
+    bias = torch.randn(c, generator=g) * 0.02
+    pos = torch.randn(1, s // p, s // p, c, generator=g) * 0.1
+    ref = torch.nn.functional.conv2d(img.float(), w.float(), bias, stride=p).permute(0, 2, 3, 1) + pos
+    out = ops.patch_embed(img.to(cuda), w.reshape(c, -1).contiguous().to(cuda), bias.to(cuda), pos[0].contiguous().to(cuda), p)
+    torch.cuda.synchronize()
+    _close(out, ref.numpy(), 2e-5)
+
+
+@pytest.mark.parametrize("b,g,cin,n", [(2, 16, 768, 256), (1, 64, 1280, 256)])
+def test_neck_convs_vs_conv(cuda, b, g, cin, n):
+    """Neck 1x1 (fp32 tokens -> fp16) and 3x3 pad-1 NHWC implicit GEMMs vs torch Conv2d (fp32 on
+    the same fp16 values; outputs rounded to fp16)."""
+    from samq import ops
+    gen = torch.Generator().manual_seed(g + cin)
+    x = torch.randn(b, g, g, cin, generator=gen)
+    w1 = (torch.randn(n, cin, 1, 1, generator=gen) * 0.03).half()
+    w2 = (torch.randn(n, n, 3, 3, generator=gen) * 0.03).half()
+    y1 = ops.conv1x1_f32(x.to(cuda), w1.reshape(n, cin).contiguous().to(cuda))
+    ref1 = torch.nn.functional.conv2d(x.half().float().permute(0, 3, 1, 2), w1.float()).permute(0, 2, 3, 1)
+    _close(y1, ref1.numpy(), 2e-3)
+    y2 = ops.conv3x3_nhwc(y1, w2.permute(0, 2, 3, 1).contiguous().to(cuda))
+    ref2 = torch.nn.functional.conv2d(y1.float().cpu().permute(0, 3, 1, 2), w2.float(), padding=1).permute(0, 2, 3, 1)
+    _close(y2, ref2.numpy(), 2e-3)
+
+
+def test_conv_ops_reject_bad_shapes(cuda):
+    from samq import ops
+    with pytest.raises((AssertionError, NotImplementedError)):
+        ops.conv1x1_f32(torch.zeros(8, 40, device=cuda), torch.zeros(128, 40, dtype=torch.float16, device=cuda))
+    with pytest.raises((AssertionError, NotImplementedError)):
+        ops.conv3x3_nhwc(torch.zeros(1, 8, 8, 48, dtype=torch.float16, device=cuda),
+                         torch.zeros(128, 3, 3, 48, dtype=torch.float16, device=cuda))
