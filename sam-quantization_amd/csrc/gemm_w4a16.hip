@@ -299,6 +299,36 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// int4 -> fp16 unpack of one packed word (8 k-values of one column, nibble order
+// [k0,k2,k4,k6 | k1,k3,k5,k7]; nibble group i at bits 4i..4i+3 of both halves).  A nibble on
+// mantissa bits 0..3 under the exponent of 1024 is the exact fp16 integer 1024+q; on bits 4..7
+// under the exponent of 64 it is 64+q.  So groups 0 and 1 convert in place and groups 2 and 3
+// after ONE shift by 8 of the word: 5 bit ops + 4 packed subtractions of (magic + zp) per 8
+// weights instead of 7 + 4.  (Bits 8..15 would reach the 5-bit exponent field.)
+struct W4Unpack {
+  uint32_t m0, m1, g0, g1;   // masks / magics, held in VGPRs (gfx950 VOP3 takes no literal)
+  __device__ void init() {
+    m0 = 0x000F000Fu; m1 = 0x00F000F0u; g0 = 0x64006400u; g1 = 0x54005400u;
+    asm volatile("" : "+v"(m0), "+v"(m1), "+v"(g0), "+v"(g1));
+  }
+};
+struct W4Zero {   // (magic + zero point) splats of one column
+  half2_t z1024, z64;
+  __device__ void set(int zp) {
+    const _Float16 a = (_Float16)(1024 + zp), b = (_Float16)(64 + zp);
+    z1024 = half2_t{a, a};
+    z64 = half2_t{b, b};
+  }
+};
+__device__ __forceinline__ half8_t w4_unpack(uint32_t w, const W4Unpack& k, const W4Zero& z) {
+  const uint32_t w8 = w >> 8;
+  const half2_t h0 = __builtin_bit_cast(half2_t, (w & k.m0) | k.g0) - z.z1024;
+  const half2_t h1 = __builtin_bit_cast(half2_t, (w & k.m1) | k.g1) - z.z64;
+  const half2_t h2 = __builtin_bit_cast(half2_t, (w8 & k.m0) | k.g0) - z.z1024;
+  const half2_t h3 = __builtin_bit_cast(half2_t, (w8 & k.m1) | k.g1) - z.z64;
+  return half8_t{h0[0], h0[1], h1[0], h1[1], h2[0], h2[1], h3[0], h3[1]};
+}
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED, int VAR = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
@@ -370,13 +400,13 @@ void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
   int col[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) col[t] = n0 + wn * WN + t * 32 + (lane & 31);
-  half2_t zc[TN], sc[TN];
+  W4Zero zc[TN];
+  half2_t sc[TN];
   auto load_zc = [&](int g) {
 #pragma unroll
     for (int t = 0; t < TN; ++t) {
       const uint32_t zw = qzeros[(int64_t)g * (N / 8) + (col[t] >> 3)];
-      const _Float16 z = (_Float16)(1024 + (int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
-      zc[t] = half2_t{z, z};
+      zc[t].set((int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
       if (GROUPED) {
         const _Float16 s = scales[(int64_t)g * N + col[t]];
         sc[t] = half2_t{s, s};
@@ -386,8 +416,8 @@ void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
   load_zc(0);
   int cur_group = 0;
 
-  uint32_t kMask = 0x000F000Fu, kMagic = 0x64006400u;
-  asm volatile("" : "+v"(kMask), "+v"(kMagic));
+  W4Unpack ku;
+  ku.init();
 
   float16_t acc[TM][TN];
 #pragma unroll
@@ -437,12 +467,14 @@ void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
         if (VAR == 1) {   // TIMING-ONLY variant (wrong results): MFMA on the raw words, no unpack
           bf = __builtin_bit_cast(half8_t, bw[t]);
         } else {
+          bf = w4_unpack(w, ku, zc[t]);
+          if (GROUPED) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            half2_t h = __builtin_bit_cast(half2_t, ((w >> (4 * i)) & kMask) | kMagic) - zc[t];
-            if (GROUPED) h = h * sc[t];
-            bf[2 * i] = h[0];
-            bf[2 * i + 1] = h[1];
+            for (int i = 0; i < 4; ++i) {
+              const half2_t h = half2_t{bf[2 * i], bf[2 * i + 1]} * sc[t];
+              bf[2 * i] = h[0];
+              bf[2 * i + 1] = h[1];
+            }
           }
         }
 #pragma unroll
@@ -866,16 +898,15 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   };
 
   int col[TN];
-  half2_t zc[TN];
+  W4Zero zc[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
     col[t] = n0 + wn * WN + t * 32 + (lane & 31);
     const uint32_t zw = qzeros[col[t] >> 3];
-    const _Float16 z = (_Float16)(1024 + (int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
-    zc[t] = half2_t{z, z};
+    zc[t].set((int)((zw >> (4 * (col[t] & 7))) & 0xFu) + 1);
   }
-  uint32_t kMask = 0x000F000Fu, kMagic = 0x64006400u;
-  asm volatile("" : "+v"(kMask), "+v"(kMagic));
+  W4Unpack ku;
+  ku.init();
 
   float16_t acc[TM][TN];
 #pragma unroll
@@ -943,13 +974,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       for (int t = 0; t < TN; ++t)
 #pragma unroll
         for (int s = 0; s < KPP; ++s) {
-          const uint32_t w = bw[t][p * KPP + s];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const half2_t h = __builtin_bit_cast(half2_t, ((w >> (4 * i)) & kMask) | kMagic) - zc[t];
-            bf[t][s][2 * i] = h[0];
-            bf[t][s][2 * i + 1] = h[1];
-          }
+          bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
         }
       if (VAR & 4) stamp(0);
       __builtin_amdgcn_sched_barrier(0);

@@ -128,3 +128,24 @@ def test_module_float_forward_matches_oracle():
         y = enc(torch.from_numpy(img)).numpy()
     ref = sam_ref.EncoderOracle(cfg, st)(img).numpy()
     assert np.abs(y - ref).max() < 1e-4
+
+
+def test_w4_unpack_bit_trick_exact():
+    """The GEMM kernels' int4 -> fp16 unpack (csrc/gemm_w4a16.hip w4_unpack): nibble groups 0/1 OR-ed
+    into the mantissa under the exponents of 1024 / 64, groups 2/3 the same after one shift by 8,
+    are the exact fp16 integers magic + q for every 32-bit word pattern tried."""
+    import numpy as np
+    rng = np.random.default_rng(0)
+    w = rng.integers(0, 2 ** 32, size=20000, dtype=np.uint64).astype(np.uint32)
+    w = np.concatenate([w, np.array([0, 0xFFFFFFFF, 0x88888888, 0x0F0F0F0F, 0xF0F0F0F0], np.uint32)])
+
+    def f16(x):
+        return np.frombuffer(np.ascontiguousarray(x, dtype=np.uint16).tobytes(), dtype=np.float16).astype(np.float32)
+
+    w8 = w >> 8
+    groups = [((w & 0x000F000F) | 0x64006400, 1024), ((w & 0x00F000F0) | 0x54005400, 64),
+              ((w8 & 0x000F000F) | 0x64006400, 1024), ((w8 & 0x00F000F0) | 0x54005400, 64)]
+    for i, (x, magic) in enumerate(groups):
+        lo, hi = f16(x & 0xFFFF) - magic, f16(x >> 16) - magic
+        assert np.array_equal(lo, (w >> (4 * i)) & 15)
+        assert np.array_equal(hi, (w >> (16 + 4 * i)) & 15)
