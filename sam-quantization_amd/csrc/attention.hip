@@ -232,12 +232,18 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
     }
   }
 
+  // SP >= 32: the softmax denominator is accumulated by the P.V MFMAs themselves (one more
+  // 16x16x32 against an all-ones A operand per 32 keys, rescaled with O) instead of one VALU add
+  // per score plus the cross-lane reduction -- the softmax VALU is what bounds this kernel.
+  constexpr bool MSUM = SP >= 32;
   float m[QT], l[QT];
-  float4_t o[QT][DT];
+  float4_t o[QT][DT], lacc[QT];
+  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     m[t] = -INFINITY;
     l[t] = 0.f;
+    lacc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int d = 0; d < DT; ++d) o[t][d] = float4_t{0.f, 0.f, 0.f, 0.f};
   }
@@ -252,41 +258,32 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
     __syncthreads();   // TH visible (the K/V ring is ordered by counted vmcnt + s_barrier below)
   }
 
-  for (int kh = 0; kh < S; ++kh) {
-    const char* kb;
-    if (RESIDENT) {
-      kb = smem + kh * S * (D * 2);
-    } else {
-      if (kh + 1 < S) wait_vmcnt<NI>(); else wait_vmcnt<0>();
-      __builtin_amdgcn_s_barrier();   // row kh landed for every wave; row kh-1 fully consumed
-      if (kh + 2 < S) issue(kh + 2, (kh + 2) % 3);
-      kb = smem + (kh % 3) * BUFB;
-    }
-    const char* vb = kb + (RESIDENT ? (UNIT_CHUNKS / 2) * 16 : ROWB);
-
-    // ---- scores S^T = K . Q^T (+ TW as the C input)
-    float4_t sc[QT][KT];
+  // ---- per key row: scores (QK), online softmax, O += P.V -- as lambdas so the streaming loop
+  // can software-pipeline them (see below)
+  using PB = half8_t[QT][(SP + 31) / 32];
+  auto qk = [&](const char* kb, float4_t (&sc)[QT][KT]) {
+      // ---- scores S^T = K . Q^T (+ TW as the C input)
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      const char* krow = kb + (kt * 16 + ql) * (D * 2);
-      half8_t kf[KS];
+      for (int kt = 0; kt < KT; ++kt) {
+        const char* krow = kb + (kt * 16 + ql) * (D * 2);
+        half8_t kf[KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        kf[s] = half8_t{};
-        if (s < 2 || kin3) kf[s] = *(const half8_t*)(krow + (32 * s + 8 * g) * 2);
+        for (int s = 0; s < KS; ++s) {
+          kf[s] = half8_t{};
+          if (s < 2 || kin3) kf[s] = *(const half8_t*)(krow + (32 * s + 8 * g) * 2);
+        }
+#pragma unroll
+        for (int t = 0; t < QT; ++t) {
+          float4_t a = tw[t][kt];
+#pragma unroll
+          for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[t][s], a, 0, 0, 0);
+          sc[t][kt] = a;
+        }
       }
-#pragma unroll
-      for (int t = 0; t < QT; ++t) {
-        float4_t a = tw[t][kt];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[t][s], a, 0, 0, 0);
-        sc[t][kt] = a;
-      }
-    }
 
+  };
+  auto soft = [&](int kh, float4_t (&sc)[QT][KT], PB& pb, half4_t (&pb16)[QT]) {
     // ---- online softmax (exp2 domain); TH[q, kh] is constant along the row
-    half8_t pb[QT][(SP + 31) / 32];
-    half4_t pb16[QT];
     bool any_rescale = false;
     float alpha[QT];
 #pragma unroll
@@ -320,9 +317,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
         for (int r = 0; r < 4; ++r) {
           const float e = __builtin_amdgcn_exp2f(sc[t][kt][r] - corr);
           sc[t][kt][r] = e;
-          rs += e;
+          if (!MSUM) rs += e;
         }
-      l[t] = l[t] * alpha[t] + rs;
+      if (!MSUM) l[t] = l[t] * alpha[t] + rs;
       if (SP == 16) {
         pb16[t] = half4_t{(_Float16)sc[t][0][0], (_Float16)sc[t][0][1], (_Float16)sc[t][0][2], (_Float16)sc[t][0][3]};
       } else {
@@ -341,8 +338,13 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
       for (int t = 0; t < QT; ++t)
 #pragma unroll
         for (int d = 0; d < DT; ++d) o[t][d] = o[t][d] * alpha[t];
+#pragma unroll
+      for (int t = 0; t < QT; ++t)
+        if (MSUM) lacc[t] = lacc[t] * alpha[t];
     }
 
+  };
+  auto pv = [&](const char* vb, PB& pb, half4_t (&pb16)[QT]) {
     // ---- O^T += V^T . P^T  (V^T fragments by hardware-transposed LDS reads of row-major V)
 #pragma unroll
     for (int d = 0; d < DT; ++d) {
@@ -375,14 +377,65 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
         }
       }
     }
+    if constexpr (MSUM) {
+      constexpr int NS = SP / 32;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int t = 0; t < QT; ++t) lacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pb[t][s], lacc[t], 0, 0, 0);
+    }
+  };
+
+  if (RESIDENT) {
+    for (int kh = 0; kh < S; ++kh) {
+      const char* kb = smem + kh * S * (D * 2);
+      float4_t sc[QT][KT];
+      PB pb;
+      half4_t pb16[QT];
+      qk(kb, sc);
+      soft(kh, sc, pb, pb16);
+      pv(kb + (UNIT_CHUNKS / 2) * 16, pb, pb16);
+    }
+  } else {
+    // Streaming (global) attention, software-pipelined by one key row: the Q.K^T MFMAs of row
+    // kh+1 are issued ahead of the softmax of row kh (independent registers), so the MFMA tail
+    // drains under the first softmax VALU work (with the MFMA row sums: 507 -> 474 us at ViT-H
+    // B=4; forcing a finer MFMA/VALU interleave with sched_group_barrier spills, and the
+    // softmax's max -> reduce -> exp chain leaves little to interleave).  Ring: row r in slot
+    // r % 3; at the top of iteration kh row kh+1 is retired (nothing newer in flight) and, after
+    // the barrier that also ends every read of row kh-1, row kh+2 is staged into row kh-1's slot.
+    float4_t scA[QT][KT], scB[QT][KT];
+    PB pb;
+    half4_t pb16[QT];
+    if (S > 1) wait_vmcnt<NI>(); else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();   // row 0 landed for every wave
+    qk(smem, scA);
+    auto step = [&](int kh, float4_t (&cur)[QT][KT], float4_t (&nxt)[QT][KT]) {
+      if (kh + 1 < S) {
+        wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();   // row kh+1 landed for every wave; row kh-1 fully consumed
+        if (kh + 2 < S) issue(kh + 2, (kh + 2) % 3);
+        qk(smem + ((kh + 1) % 3) * BUFB, nxt);
+      }
+      soft(kh, cur, pb, pb16);
+      pv(smem + (kh % 3) * BUFB + ROWB, pb, pb16);
+    };
+    for (int kh = 0; kh < S; kh += 2) {   // S is even on this path (32 or 64)
+      step(kh, scA, scB);
+      step(kh + 1, scB, scA);
+    }
   }
 
   // ---------------------------------------------------------------- normalise + store
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
     float lt = l[t];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    if (MSUM) {
+      lt = lacc[t][0];
+    } else {
+      lt += __shfl_xor(lt, 16, 64);
+      lt += __shfl_xor(lt, 32, 64);
+    }
     const int x = qcol0[t] + ql;
     if (tok_kind(qrow[t], x) != 0) continue;
     const float inv = 1.0f / lt;
