@@ -796,7 +796,7 @@ template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
   int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   int grid = cus < items ? cus : items;
   grid = (grid + 7) & ~7;   // multiple of 8 (XCD-aware item numbering); surplus workgroups exit
   hipLaunchKernelGGL((win_attention_kernel<D>), dim3(grid), dim3(64 * 7), 0, stream, p, items);
