@@ -124,6 +124,21 @@ int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked
 #define SAMQ_Q_OUT_FQ 2
 int samq_quantize(const void* x, void* y, int64_t n, float scale, int flags, hipStream_t stream);
 
+/* Running min / max of a calibration tensor viewed as (rows, C) row-major -- fq_vit
+ * MinmaxObserver.update (observer/minmax.py:14-29, reshape_tensor observer/base.py:16-29):
+ *   SAMQ_MM_PER_ROW: one value per row     (conv / linear weights, v.reshape(out, -1));
+ *   SAMQ_MM_PER_COL: one value per column  (channel-last activations, channel_wise);
+ *   SAMQ_MM_ALL:     one scalar            (layer_wise).
+ * x f32 (f16 with in_f16); max_io / min_io f32 (rows, C or 1 values): overwritten when init != 0,
+ * else merged with max(old, new) / min(old, new).  NaN propagates as in torch.max / torch.min.
+ * PER_COL and ALL need a float workspace of samq_minmax_workspace(rows, C, axis) elements. */
+#define SAMQ_MM_PER_ROW 0
+#define SAMQ_MM_PER_COL 1
+#define SAMQ_MM_ALL 2
+size_t samq_minmax_workspace(int64_t rows, int C, int axis);
+int samq_minmax(const void* x, int64_t rows, int C, int in_f16, int axis, float* max_io, float* min_io,
+                int init, float* workspace, size_t workspace_floats, hipStream_t stream);
+
 /* Gated-MLP activation: out f16[i] = silu(gate[i]) * up[i] (f32 inputs).  With two
  * samq_w4a16_gemm(..., SAMQ_EPI_F32) calls it replaces triton_llama_mlp_4 /
  * llama_mlp_fused_4_kernel (gptq_triton/fused_mlp.py:391-477, 230-388). */

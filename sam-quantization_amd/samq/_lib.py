@@ -31,6 +31,9 @@ BF_W4 = 1
 Q_IN_F16 = 1
 Q_OUT_FQ = 2
 
+MM_PER_ROW = 0
+MM_PER_COL = 1
+MM_ALL = 2
 LN_IN_F16 = 1
 LN_OUT_F32 = 2
 LN_IN_I8 = 4
@@ -58,6 +61,8 @@ SIGNATURES = {
     "samq_i8_gemm_cfg": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
                                 _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "samq_quantize": (_i32, [_vp, _vp, _i64, _f32, _i32, _vp]),
+    "samq_minmax_workspace": (ctypes.c_size_t, [_i64, _i32, _i32]),
+    "samq_minmax": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, ctypes.c_size_t, _vp]),
     "samq_silu_mul": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
     "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),

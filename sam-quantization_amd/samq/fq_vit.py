@@ -124,6 +124,8 @@ class MinmaxObserver:
         return v.reshape(-1, v.shape[-1]).transpose(0, 1)
 
     def update(self, v: torch.Tensor) -> None:
+        if v.is_cuda:
+            return self._update_hip(v)
         v = self.reshape_tensor(v)
         cur_max, cur_min = v.max(dim=1).values, v.min(dim=1).values
         self.max_val = cur_max if self.max_val is None else torch.max(cur_max, self.max_val)
@@ -131,6 +133,34 @@ class MinmaxObserver:
         if self.calibration_mode == "layer_wise":
             self.max_val = self.max_val.max()
             self.min_val = self.min_val.min()
+
+    def _update_hip(self, v: torch.Tensor) -> None:
+        """GPU tensors: the same statistics from one HIP reduction (``samq_minmax``) on the
+        un-transposed layout -- rows of ``(out, -1)`` for weights, columns of the channel-last
+        ``(-1, C)`` view for activations, everything for layer_wise.  Bit-identical to the torch
+        path (max / min are exact); running values are f32 for f32 / f16 / bf16 inputs alike
+        (the torch path keeps the input dtype: same values, as the inputs convert exactly)."""
+        from . import ops, _lib
+        v = v.detach()
+        if v.dtype not in (torch.float32, torch.float16):
+            v = v.float()
+        if self.module_type in ("conv_weight", "linear_weight"):
+            x2d = v.reshape(v.shape[0], -1).contiguous()
+            per = _lib.MM_PER_ROW
+        else:
+            if v.dim() == 4 and self.permute:
+                v = v.permute(0, 2, 3, 1)
+            x2d = v.reshape(-1, v.shape[-1]).contiguous()
+            per = _lib.MM_PER_COL
+        axis = _lib.MM_ALL if self.calibration_mode == "layer_wise" else per
+        if self.max_val is not None:
+            want = () if axis == _lib.MM_ALL else (x2d.shape[0] if per == _lib.MM_PER_ROW else x2d.shape[1],)
+            if tuple(self.max_val.shape) != want or self.max_val.dtype != torch.float32 or not self.max_val.is_cuda:
+                raise ValueError(f"MinmaxObserver: running statistics of shape {tuple(self.max_val.shape)} "
+                                 f"do not match this tensor's {want}")
+            self.max_val, self.min_val = ops.minmax_update(x2d, axis, self.max_val.clone(), self.min_val.clone())
+        else:
+            self.max_val, self.min_val = ops.minmax_update(x2d, axis)
 
     def get_quantization_params(self, *args, **kwargs):
         qmax, qmin = self.bit_type.upper_bound, self.bit_type.lower_bound

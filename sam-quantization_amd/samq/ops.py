@@ -191,6 +191,30 @@ def quantize(x: torch.Tensor, scale: float, fake: bool = False, out: Optional[to
     return out
 
 
+def minmax_update(x2d: torch.Tensor, axis: int, max_val: Optional[torch.Tensor] = None,
+                  min_val: Optional[torch.Tensor] = None):
+    """fq_vit ``MinmaxObserver.update`` core on the GPU (``samq_minmax``): running max / min of a
+    contiguous (rows, C) f32 / f16 tensor per row (``MM_PER_ROW``), per column (``MM_PER_COL``)
+    or over everything (``MM_ALL``, 0-dim results).  ``max_val`` / ``min_val`` None -> fresh f32
+    tensors; else they are merged in place (f32, contiguous, matching shape)."""
+    _need_cuda(x2d)
+    assert x2d.dim() == 2 and x2d.is_contiguous() and x2d.dtype in (torch.float32, torch.float16)
+    rows, c = x2d.shape
+    shape = {_lib.MM_PER_ROW: (rows,), _lib.MM_PER_COL: (c,), _lib.MM_ALL: ()}[axis]
+    init = max_val is None
+    if init:
+        max_val = torch.empty(shape, dtype=torch.float32, device=x2d.device)
+        min_val = torch.empty(shape, dtype=torch.float32, device=x2d.device)
+    for t in (max_val, min_val):
+        assert t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == shape and t.device == x2d.device
+    lib = _lib.load()
+    nws = lib.samq_minmax_workspace(rows, c, axis)
+    ws = torch.empty(max(nws, 1), dtype=torch.float32, device=x2d.device)
+    _lib.check(lib.samq_minmax(_ptr(x2d), rows, c, int(x2d.dtype == torch.float16), axis, _ptr(max_val),
+                               _ptr(min_val), int(init), _ptr(ws), nws, _stream()), "minmax")
+    return max_val, min_val
+
+
 def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, in_scale: float = 0.0,
                 out_scale: float = 0.0, out_dtype: torch.dtype = torch.int8,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
