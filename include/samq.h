@@ -223,6 +223,12 @@ int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float*
 int samq_patch_embed(const void* img, const void* weight, const float* bias, const float* pos, float* out,
                      int B, int Cin, int img_size, int patch, int N, hipStream_t stream);
 
+/* The same in fp32 end to end (img f32, weight f32, fp32 MFMA): the W4A8 encoder's patch
+ * embedding, whose int8 quantiser follows directly (fq_vit image_encoder.py PatchEmbed + QAct).
+ * patch % 4 == 0, Cin*p*p % 16 == 0, N % 128 == 0. */
+int samq_patch_embed_f32(const float* img, const float* weight, const float* bias, const float* pos,
+                         float* out, int B, int Cin, int img_size, int patch, int N, hipStream_t stream);
+
 /* Neck 1x1 conv, no bias (image_encoder.py:88-104 neck[0]) on the fp32 token rows:
  * x f32 [M, K] (converted to f16 on load, as the reference's fp16 neck), weight f16 [N, K]
  * -> out f16 [M, N].  K % 32 == 0, N % 128 == 0. */

@@ -155,6 +155,108 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 }
 
+// fp32 patch embedding (the W4A8 engine: its first int8 quantiser sits right behind it, so the
+// embedding keeps the reference's fp32 arithmetic): the same implicit GEMM on
+// v_mfma_f32_32x32x2_f32, 128x128x16 tiles, fp32 image / weight / accumulation.
+__global__ __launch_bounds__(256) void patch_embed_f32_kernel(ConvArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 16;
+  constexpr int PITCH = BK + 1;   // floats; odd pitch spreads a fragment's 32 rows over the banks
+  constexpr int BUF = (BM + BN) * PITCH;
+  __shared__ float smem[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = a.K / BK;
+  const int gg = a.G * a.G, pp = a.P * a.P, side = a.G * a.P;
+
+  // staging: float4 chunk c = tid + 256 j (j = 0, 1) -> row c / 4, 4 k-values at (c % 4) * 4
+  float4_t ra[2], rb[2];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, k = kt * BK + (c & 3) * 4;
+      int t = m0 + row;
+      t = t < a.M ? t : a.M - 1;
+      const int b = t / gg, gy = (t / a.G) % a.G, gx = t % a.G;
+      const int ci = k / pp, rem = k - ci * pp, kh = rem / a.P, kw = rem - kh * a.P;
+      ra[j] = *(const float4_t*)((const float*)a.x + (((int64_t)b * a.Cin + ci) * side + gy * a.P + kh) * side +
+                                 gx * a.P + kw);
+      rb[j] = *(const float4_t*)((const float*)a.w + (int64_t)(n0 + row) * a.K + k);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, off = (c & 3) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        smem[buf * BUF + row * PITCH + off + e] = ra[j][e];
+        smem[buf * BUF + (BM + row) * PITCH + off + e] = rb[j][e];
+      }
+    }
+  };
+
+  float16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0.f;
+
+  const int hsel = lane >> 5;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < kt_count) load(kt + 1);
+    const float* base = smem + buf * BUF;
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      float af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = base[(wm * 64 + i * 32 + (lane & 31)) * PITCH + 2 * s + hsel];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) bf[t] = base[(BM + wn * 64 + t * 32 + (lane & 31)) * PITCH + 2 * s + hsel];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[t], acc[i][t], 0, 0, 0);
+    }
+    if (kt + 1 < kt_count) {
+      store(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = n0 + wn * 64 + t * 32 + (lane & 31);
+    const float bcol = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        if (row >= a.M) continue;
+        float v = acc[i][t][r] + bcol;
+        if (a.pos) v += a.pos[(int64_t)(row % gg) * a.N + col];
+        ((float*)a.out)[(int64_t)row * a.N + col] = v;
+      }
+    }
+  }
+}
+
 template <int MODE>
 static int conv_launch(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + 127) / 128) * (a.N / 128);
@@ -204,4 +306,22 @@ extern "C" int samq_conv3x3_nhwc(const void* x, const void* weight, void* out, i
                "conv3x3: operands must be 16-byte aligned");
   ConvArgs a{x, (const _Float16*)weight, nullptr, nullptr, out, B * G * G, N, 9 * Cin, G, 1, Cin};
   return conv_launch<CG_3X3>(a, stream);
+}
+
+extern "C" int samq_patch_embed_f32(const float* img, const float* weight, const float* bias, const float* pos,
+                                    float* out, int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  SAMQ_REQUIRE(img && weight && out, SAMQ_ERR_INVALID, "patch_embed_f32: null pointer");
+  SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
+               "patch_embed_f32: image size must be a multiple of the patch size");
+  SAMQ_REQUIRE(patch % 4 == 0 && (Cin * patch * patch) % 16 == 0, SAMQ_ERR_UNSUPPORTED,
+               "patch_embed_f32: patch must be a multiple of 4 and Cin*patch^2 a multiple of 16");
+  SAMQ_REQUIRE(N % 128 == 0, SAMQ_ERR_UNSUPPORTED, "patch_embed_f32: embed dim must be a multiple of 128");
+  SAMQ_REQUIRE(((uintptr_t)img & 15) == 0 && ((uintptr_t)weight & 15) == 0, SAMQ_ERR_INVALID,
+               "patch_embed_f32: image and weight must be 16-byte aligned");
+  const int g = img_size / patch;
+  ConvArgs a{img, (const _Float16*)weight, bias, pos, out, B * g * g, N, Cin * patch * patch, g, patch, Cin};
+  const int nwg = ((a.M + 127) / 128) * (a.N / 128);
+  hipLaunchKernelGGL(patch_embed_f32_kernel, dim3(nwg), dim3(256), 0, stream, a);
+  SAMQ_LAUNCH_CHECK("patch_embed_f32 launch");
+  return SAMQ_OK;
 }

@@ -140,25 +140,16 @@ class EncoderEngine:
     # ---------------------------------------------------------------- stages
     def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
         """Patch embedding + bias + pos_embed into the fp32 residual stream: one implicit-GEMM HIP
-        kernel (patches read straight from the NCHW image).  W4A8 computes it in fp32 (vendor GEMM,
-        one per image so an image's result does not depend on its batch): its first int8
-        quantiser sits right behind it."""
-        b = img.shape[0]
-        p, g = self.patch, self.grid
+        kernel (patches read straight from the NCHW image).  W4A8 computes it in fp32
+        (``samq_patch_embed_f32``): its first int8 quantiser sits right behind it."""
+        p = self.patch
+        pos = None if self.pos is None else self.pos[0]
         if not self.w4a8:
-            ops.patch_embed(img.to(torch.float16).contiguous(), self.pe_w, self.pe_b,
-                            None if self.pos is None else self.pos[0], p, out=x32)
+            ops.patch_embed(img.to(torch.float16).contiguous(), self.pe_w, self.pe_b, pos, p, out=x32)
             return
-        dt = torch.float32 if self.w4a8 else torch.float16
-        w = self.pe_w.to(dt) if self.w4a8 else self.pe_w
-        cols = img.to(dt).reshape(b, -1, g, p, g, p).permute(0, 2, 4, 1, 3, 5).reshape(b, g * g, -1)
-        for i in range(b):
-            y = torch.matmul(cols[i], w.t()).float().view(g, g, -1)
-            if self.pe_b is not None:
-                y = y + self.pe_b
-            if self.pos is not None:
-                y = y + self.pos[0]
-            x32[i].copy_(y)
+        if getattr(self, "pe_w32", None) is None:
+            self.pe_w32 = self.pe_w.float().contiguous()
+        ops.patch_embed(img.to(torch.float32).contiguous(), self.pe_w32, self.pe_b, pos, p, out=x32)
 
     def block_w4a8(self, p: _BlockPlan, bufs) -> None:
         """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded

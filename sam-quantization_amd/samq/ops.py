@@ -100,20 +100,24 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
 def patch_embed(img: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], pos: Optional[torch.Tensor],
                 patch: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """img f16 (B, Cin, S, S) -> f32 (B, S/p, S/p, N) = Conv2d(k=p, stride=p)(img) + bias + pos;
-    weight f16 (N, Cin*p*p), bias f32 (N,), pos f32 (S/p, S/p, N) or None."""
+    weight f16 (N, Cin*p*p), bias f32 (N,), pos f32 (S/p, S/p, N) or None.  With img and weight
+    both f32 the whole GEMM runs in fp32 (``samq_patch_embed_f32``, the W4A8 embedding)."""
     _need_cuda(img, weight, bias, pos)
     b, cin, s, s2 = img.shape
-    assert s == s2 and img.dtype == torch.float16 and img.is_contiguous()
+    f32 = img.dtype == torch.float32
+    dt = torch.float32 if f32 else torch.float16
+    assert s == s2 and img.dtype == dt and img.is_contiguous()
     n = weight.shape[0]
-    assert weight.dtype == torch.float16 and weight.is_contiguous() and weight.shape[1] == cin * patch * patch
+    assert weight.dtype == dt and weight.is_contiguous() and weight.shape[1] == cin * patch * patch
     assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
     assert pos is None or (pos.dtype == torch.float32 and pos.is_contiguous() and pos.numel() == (s // patch) ** 2 * n)
     g = s // patch
     if out is None:
         out = torch.empty((b, g, g, n), dtype=torch.float32, device=img.device)
     assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == b * g * g * n
-    _lib.check(_lib.load().samq_patch_embed(_ptr(img), _ptr(weight), _ptr(bias), _ptr(pos), _ptr(out), b, cin, s,
-                                            patch, n, _stream()), "patch_embed")
+    fn = _lib.load().samq_patch_embed_f32 if f32 else _lib.load().samq_patch_embed
+    _lib.check(fn(_ptr(img), _ptr(weight), _ptr(bias), _ptr(pos), _ptr(out), b, cin, s, patch, n, _stream()),
+               "patch_embed")
     return out
 
 

@@ -257,6 +257,25 @@ def test_patch_embed_vs_conv(cuda):
     _close(out, ref.numpy(), 2e-5)
 
 
+@pytest.mark.parametrize("b,s,c", [(2, 256, 768), (1, 1024, 1280)])
+def test_patch_embed_f32_vs_conv(cuda, b, s, c):
+    """fp32 PatchEmbed (the W4A8 embedding, fp32 MFMA) vs torch Conv2d in float64 on the same
+    fp32 values: fp32 rounding of a 768-term sum only."""
+    from samq import ops
+    g = torch.Generator().manual_seed(s + c)
+    p = 16
+    img = torch.randn(b, 3, s, s, generator=g)
+    w = torch.randn(c, 3, p, p, generator=g) * 0.02
+    bias = torch.randn(c, generator=g) * 0.02
+    pos = torch.randn(1, s // p, s // p, c, generator=g) * 0.1
+    ref = (torch.nn.functional.conv2d(img.double(), w.double(), bias.double(), stride=p).permute(0, 2, 3, 1)
+           + pos.double())
+    out = ops.patch_embed(img.to(cuda), w.reshape(c, -1).contiguous().to(cuda), bias.to(cuda),
+                          pos[0].contiguous().to(cuda), p)
+    torch.cuda.synchronize()
+    _close(out, ref.float().numpy(), 2e-6)
+
+
 @pytest.mark.parametrize("b,g,cin,n", [(2, 16, 768, 256), (1, 64, 1280, 256)])
 def test_neck_convs_vs_conv(cuda, b, g, cin, n):
     """Neck 1x1 (fp32 tokens -> fp16) and 3x3 pad-1 NHWC implicit GEMMs vs torch Conv2d (fp32 on
