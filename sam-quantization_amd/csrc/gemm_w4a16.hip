@@ -329,6 +329,68 @@ __device__ __forceinline__ half8_t w4_unpack(uint32_t w, const W4Unpack& k, cons
   return half8_t{h0[0], h0[1], h1[0], h1[1], h2[0], h2[1], h3[0], h3[1]};
 }
 
+// The same epilogue for 16x16x32 accumulators (VAR & 16 of the ping-pong kernel): lane (ql, g)
+// of 16-row tile i, 32-column block t, half h holds rows 16i + 4g + r of column 32t + 16h + ql;
+// staged per 16-row tile with a padded pitch (WN + 4 floats: the four lane groups' rows land
+// on different banks).
+template <int TM16, int TN, int EPI>
+__device__ __forceinline__ void pp_epilogue16(const float4_t (&acc)[TM16][TN][2], const float (&csc)[TN][2],
+                                              const float (&cb)[TN][2], char* ep_bytes, void* Cout, int64_t ldc,
+                                              int M, int row_base, int col_base, int lane) {
+  constexpr int WN = TN * 32, EP_ROWS = 16, PITCH = WN + 4;
+  float* ep = (float*)ep_bytes;
+  const int ql = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TM16; ++i) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][t][h][r] * csc[t][h] + cb[t][h];
+          if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast(v);
+          ep[(4 * g + r) * PITCH + 32 * t + 16 * h + ql] = v;
+        }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
+    const int srow0 = row_base + i * 16;
+    if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+      constexpr int C4 = WN / 4;
+#pragma unroll
+      for (int j = 0; j < (EP_ROWS * C4 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < EP_ROWS * C4) {
+          const int rl = idx / C4, c4 = idx % C4;
+          const int row = srow0 + rl;
+          const float4_t v = *(const float4_t*)(ep + rl * PITCH + 4 * c4);
+          if (row < M) {
+            float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
+            if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+          }
+        }
+      }
+    } else {
+      constexpr int C8 = WN / 8;
+#pragma unroll
+      for (int j = 0; j < (EP_ROWS * C8 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < EP_ROWS * C8) {
+          const int rl = idx / C8, c8 = idx % C8;
+          const int row = srow0 + rl;
+          const float4_t v0 = *(const float4_t*)(ep + rl * PITCH + 8 * c8);
+          const float4_t v1 = *(const float4_t*)(ep + rl * PITCH + 8 * c8 + 4);
+          if (row < M) {
+            const half8_t hv = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                                (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+            *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = hv;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // reads done before the next slice overwrites
+  }
+}
+
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, bool GROUPED, int VAR = 0>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void w4a16_gemm_v3(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
@@ -844,9 +906,14 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // phases may restage (WAR).  The retire wait for tile kt+1 sits in the load half of the last
   // phase, before the barrier after which the first group reads it (RAW).
   constexpr int PRE_LAST = pp2_pre(NPH - 1, NPW, NPH, 0);
+  // VAR & 16: v_mfma_f32_16x16x32_f16 fragments (same tile, LDS bytes and unpack count; the chip
+  // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
+  constexpr bool M16 = (VAR & 16) != 0;
+  constexpr int KS32 = 2 / NPH;                  // M16: k32 steps per phase
   constexpr int EP_ROWS = WN > 64 ? 16 : 32;
-  constexpr int EP_BYTES = EP_ROWS * WN * 4;
+  constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : EP_ROWS * WN * 4;
   constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
+  static_assert(!M16 || NPH <= 2, "M16: one or two phases per K tile");
   static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
   static_assert(LA >= 2 && LA < STAGES, "ring");
   static_assert((LA - 2) * NPW + PRE_LAST <= 63, "vmcnt");
@@ -925,6 +992,34 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     a_swz[i] = (rr >> 1) & 7;
   }
 
+  // M16 state: 16-row tiles i, column halves h of each 32-column block t; lane (ql, g16) holds
+  // column 32t + 16h + ql and k = 32 s + 8 g16 .. +7, whose packed word (layout 1: column c,
+  // k chunk kb at word kb / 2 of lane c + 32 (kb & 1)) is word 2 s + (g16 >> 1) of lane
+  // 16h + ql + 32 (g16 & 1) in the staged B block
+  const int ql = lane & 15, g16 = lane >> 4;
+  float4_t acc16[M16 ? 2 * TM : 1][TN][2];
+  W4Zero zc16[TN][2];
+  int a_off16[M16 ? 2 * TM : 1], a_swz16[M16 ? 2 * TM : 1];
+  if constexpr (M16) {
+#pragma unroll
+    for (int i = 0; i < 2 * TM; ++i) {
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc16[i][t][h] = float4_t{0.f, 0.f, 0.f, 0.f};
+      const int rr = wm * WM + i * 16 + ql;
+      a_off16[i] = rr * ROWB;
+      a_swz16[i] = (rr >> 1) & 7;
+    }
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = n0 + wn * WN + 32 * t + 16 * h + ql;
+        zc16[t][h].set((int)((qzeros[c >> 3] >> (4 * (c & 7))) & 0xFu) + 1);
+      }
+  }
+
   // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
   const int pro = kt_count < LA ? kt_count : LA;
 #pragma unroll
@@ -949,6 +1044,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     const bool pf = ahead < kt_count && !(VAR & 1);   // VAR & 1: timing-only, no restaging
     const int sa = slot + LA >= STAGES ? slot + LA - STAGES : slot + LA;   // (kt + LA) % STAGES
     u32x4 bw[TN];
+    uint32_t bw16[TN][2][2];
 #pragma unroll
     for (int p = 0; p < NPH; ++p) {
       // ---------------- load half
@@ -959,23 +1055,46 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
         for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
         vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
       }
-      if (p == 0) {
+      if (M16 && p == 0) {
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const char* bp = st + A_BYTES + (wn * TN + t) * 1024 + (16 * h + ql + 32 * (g16 & 1)) * 16 + 4 * (g16 >> 1);
+            bw16[t][h][0] = *(const uint32_t*)bp;         // k32 step 0
+            bw16[t][h][1] = *(const uint32_t*)(bp + 8);   // k32 step 1
+          }
+      } else if (p == 0) {
 #pragma unroll
         for (int t = 0; t < TN; ++t) bw[t] = *(const u32x4*)(st + A_BYTES + (wn * TN + t) * 1024 + lane * 16);
       }
-      half8_t af[TM][KPP];
+      half8_t af16[M16 ? 2 * TM : 1][KS32], bf16[TN][2][KS32];
+      if constexpr (M16) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int s = 0; s < KS32; ++s) {
+          const int k32 = p * KS32 + s;
 #pragma unroll
-        for (int s = 0; s < KPP; ++s)
-          af[i][s] = *(const half8_t*)(st + a_off[i] + (((2 * (p * KPP + s) + hsel) ^ a_swz[i]) << 4));
-      half8_t bf[TN][KPP];
+          for (int i = 0; i < 2 * TM; ++i)
+            af16[i][s] = *(const half8_t*)(st + a_off16[i] + (((4 * k32 + g16) ^ a_swz16[i]) << 4));
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
+          for (int t = 0; t < TN; ++t)
 #pragma unroll
-        for (int s = 0; s < KPP; ++s) {
-          bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
+            for (int h = 0; h < 2; ++h) bf16[t][h][s] = w4_unpack(bw16[t][h][k32], ku, zc16[t][h]);
         }
+      }
+      half8_t af[TM][KPP];
+      half8_t bf[TN][KPP];
+      if constexpr (!M16) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int s = 0; s < KPP; ++s)
+            af[i][s] = *(const half8_t*)(st + a_off[i] + (((2 * (p * KPP + s) + hsel) ^ a_swz[i]) << 4));
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int s = 0; s < KPP; ++s) bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
+      }
       if (VAR & 4) stamp(0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -983,18 +1102,30 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       if (VAR & 4) stamp(1);
       // ---------------- MFMA half
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (M16) {
 #pragma unroll
-      for (int s = 0; s < KPP; ++s)
+        for (int s = 0; s < KS32; ++s)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < 2 * TM; ++i)
 #pragma unroll
-          for (int t = 0; t < TN; ++t) {
-            if (VAR & 2) {   // timing-only: no MFMA
-              acc[i][t][0] += (float)af[i][s][0] * (float)bf[t][s][1];
-            } else {
-              acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+            for (int t = 0; t < TN; ++t)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                acc16[i][t][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af16[i][s], bf16[t][h][s], acc16[i][t][h], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < KPP; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int t = 0; t < TN; ++t) {
+              if (VAR & 2) {   // timing-only: no MFMA
+                acc[i][t][0] += (float)af[i][s][0] * (float)bf[t][s][1];
+              } else {
+                acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+              }
             }
-          }
+      }
       // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
       // the barrier otherwise; WAR-safe in every phase: see header)
       if (pf) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
@@ -1014,6 +1145,21 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     atomicAdd(&g_pp_stamps[4], (unsigned long long)kt_count * NPH);
   }
 
+  if constexpr (M16) {
+    float csc16[TN][2], cb16[TN][2];
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = n0 + wn * WN + 32 * t + 16 * h + ql;
+        csc16[t][h] = (float)scales[c];
+        cb16[t][h] = bias ? (float)bias[c] : 0.0f;
+      }
+    __syncthreads();
+    pp_epilogue16<2 * TM, TN, EPI>(acc16, csc16, cb16, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
+                                   n0 + wn * WN, lane);
+    return;
+  }
   float csc[TN], cb[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
@@ -1079,6 +1225,9 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 58: return launch_pp2<2, 4, 2, 1, 4, 2, EPI>(a, st);   // 1 phase / K tile, 4 slots, lookahead 2
       case 60: return launch_pp2<1, 8, 1, 2, 4, 3, EPI>(a, st);   // 1x8 waves (256x32 each): B unpacked once
       case 61: return launch_pp2<1, 8, 1, 4, 4, 3, EPI>(a, st);   // 1x8 waves, 4 k-phases
+      case 62: return launch_pp2<4, 2, 4, 2, 4, 3, EPI>(a, st);   // 4x2 waves (64x128 each): A read 2x, B 4x
+      case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16>(a, st);  // cfg 57 on 16x16x32 MFMA
+      case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1152,7 +1301,7 @@ static int cfg_bn(int cfg) {
                  case 31: return 320; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
                  case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
-                 case 60: return 256; case 61: return 256;
+                 case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }
 }

@@ -98,7 +98,7 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
         _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
 
 
-@pytest.mark.parametrize("cfg", [55, 56, 57, 58])
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
