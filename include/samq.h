@@ -153,6 +153,8 @@ int samq_silu_mul(const float* gate, const float* up, void* out, int64_t n, hipS
  * channel LayerNorm2d of the neck on NHWC tokens (segment_anything/modeling/common.py:31-43). */
 #define SAMQ_LN_IN_F16 1
 #define SAMQ_LN_OUT_F32 2
+/* tuning: rows per wave (1, 2 or 4; 0 = the library default) in bits 16-18 of flags */
+#define SAMQ_LN_RPW(n) ((n) << 16)
 int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
                    int C, float eps, int flags, hipStream_t stream);
 

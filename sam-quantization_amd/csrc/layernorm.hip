@@ -14,72 +14,83 @@ __device__ __forceinline__ float ln_q8(float v, float s) {
   return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);   // fq_vit uniform.py:31-36
 }
 
-template <int IN, int OUT, int VPT>  // VPT = 4-channel vectors per lane
+template <int IN, int OUT, int VPT, int RPW>  // VPT = 4-channel vectors per lane, RPW = rows per wave
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ xin, void* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows, int C,
                                                         float eps, float in_scale, float out_scale) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= rows) return;
   const int nvec = C / 4;
-  float4_t v[VPT];
-  float s = 0.f;
+  // all RPW rows' loads are issued before the first reduction: RPW x VPT 16-byte loads in flight
+  float4_t v[RPW][VPT];
 #pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int j = lane + 64 * i;
-    if (j < nvec) {
-      if (IN == LN_F16) {
-        const half4_t h = ((const half4_t*)xin)[row * nvec + j];
-        v[i] = float4_t{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
-      } else if (IN == LN_I8) {
-        const uint32_t w = ((const uint32_t*)xin)[row * nvec + j];
+  for (int r = 0; r < RPW; ++r) {
+    const int64_t row = row0 + r < rows ? row0 + r : rows - 1;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[i][e] = (float)(int8_t)((w >> (8 * e)) & 0xFFu) * in_scale;
+    for (int i = 0; i < VPT; ++i) {
+      const int j = lane + 64 * i;
+      if (j < nvec) {
+        if (IN == LN_F16) {
+          const half4_t h = ((const half4_t*)xin)[row * nvec + j];
+          v[r][i] = float4_t{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+        } else if (IN == LN_I8) {
+          const uint32_t w = ((const uint32_t*)xin)[row * nvec + j];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[r][i][e] = (float)(int8_t)((w >> (8 * e)) & 0xFFu) * in_scale;
+        } else {
+          v[r][i] = ((const float4_t*)xin)[row * nvec + j];
+        }
       } else {
-        v[i] = ((const float4_t*)xin)[row * nvec + j];
-      }
-      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
-    } else {
-      v[i] = float4_t{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  const float mean = wave_sum(s) / (float)C;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int j = lane + 64 * i;
-    if (j < nvec) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float d = v[i][e] - mean;
-        q += d * d;
+        v[r][i] = float4_t{0.f, 0.f, 0.f, 0.f};
       }
     }
   }
-  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
 #pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int j = lane + 64 * i;
-    if (j < nvec) {
-      const float4_t g = ((const float4_t*)gamma)[j];
-      const float4_t b = ((const float4_t*)beta)[j];
-      float4_t o;
+  for (int r = 0; r < RPW; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) break;
+    float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * g[e] + b[e];
-      if (OUT == LN_F32) {
-        ((float4_t*)y)[row * nvec + j] = o;
-      } else if (OUT == LN_FQ32) {
+    for (int i = 0; i < VPT; ++i) s += v[r][i][0] + v[r][i][1] + v[r][i][2] + v[r][i][3];
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = ln_q8(o[e], out_scale) * out_scale;
-        ((float4_t*)y)[row * nvec + j] = o;
-      } else if (OUT == LN_I8) {
-        uint32_t w = 0;
+    for (int i = 0; i < VPT; ++i) {
+      const int j = lane + 64 * i;
+      if (j < nvec) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)ln_q8(o[e], out_scale) & 0xFFu) << (8 * e);
-        ((uint32_t*)y)[row * nvec + j] = w;
-      } else {
-        ((half4_t*)y)[row * nvec + j] = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[r][i][e] - mean;
+          q += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int j = lane + 64 * i;
+      if (j < nvec) {
+        const float4_t g = ((const float4_t*)gamma)[j];
+        const float4_t b = ((const float4_t*)beta)[j];
+        float4_t o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (v[r][i][e] - mean) * rstd * g[e] + b[e];
+        if (OUT == LN_F32) {
+          ((float4_t*)y)[row * nvec + j] = o;
+        } else if (OUT == LN_FQ32) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = ln_q8(o[e], out_scale) * out_scale;
+          ((float4_t*)y)[row * nvec + j] = o;
+        } else if (OUT == LN_I8) {
+          uint32_t w = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)ln_q8(o[e], out_scale) & 0xFFu) << (8 * e);
+          ((uint32_t*)y)[row * nvec + j] = w;
+        } else {
+          ((half4_t*)y)[row * nvec + j] = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+        }
       }
     }
   }
@@ -89,20 +100,35 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 
 using namespace samq;
 
+// rows per wave: SAMQ_LN_RPW(n) in flags (0 = default; rows wider than 1280 channels use 1)
+#define SAMQ_LN_DEFAULT_RPW 2   // measured: ViT-H rows 33.0 -> 27.3 us uncached (tools/bench_ln.py)
+static int ln_rpw(int flags) {
+  const int r = (flags >> 16) & 7;
+  return r == 0 ? SAMQ_LN_DEFAULT_RPW : r;
+}
+
 static int ln_launch(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C, float eps,
-                     int in, int out, float in_scale, float out_scale, hipStream_t stream) {
+                     int in, int out, float in_scale, float out_scale, int rpw, hipStream_t stream) {
   SAMQ_REQUIRE(x && y && gamma && beta, SAMQ_ERR_INVALID, "layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 4096, SAMQ_ERR_INVALID, "layernorm: C must be a multiple of 4, <= 4096");
   if (rows <= 0) return SAMQ_OK;
-  const dim3 grid((unsigned)((rows + 3) / 4));
+  SAMQ_REQUIRE(rpw == 1 || rpw == 2 || rpw == 4, SAMQ_ERR_INVALID, "layernorm: rows per wave must be 1, 2 or 4");
   const int vpt = (C / 4 + 63) / 64;
+  if (vpt > 5) rpw = 1;
+  const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
+#define LN_R(I, O, V) \
+  do { \
+    if (rpw == 1) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 2>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    else hipLaunchKernelGGL((layernorm_kernel<I, O, V, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+  } while (0)
 #define LN_V(I, O) \
   do { \
-    if (vpt <= 1) hipLaunchKernelGGL((layernorm_kernel<I, O, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else if (vpt <= 3) hipLaunchKernelGGL((layernorm_kernel<I, O, 3>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else if (vpt <= 4) hipLaunchKernelGGL((layernorm_kernel<I, O, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else if (vpt <= 5) hipLaunchKernelGGL((layernorm_kernel<I, O, 5>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else hipLaunchKernelGGL((layernorm_kernel<I, O, 16>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    if (vpt <= 1) LN_R(I, O, 1); \
+    else if (vpt <= 3) LN_R(I, O, 3); \
+    else if (vpt <= 4) LN_R(I, O, 4); \
+    else if (vpt <= 5) LN_R(I, O, 5); \
+    else LN_R(I, O, 16); \
   } while (0)
 #define LN_O(I) \
   do { \
@@ -112,6 +138,7 @@ static int ln_launch(const void* x, void* y, const float* gamma, const float* be
   switch (in) { case LN_F16: LN_O(LN_F16); break; case LN_I8: LN_O(LN_I8); break; default: LN_O(LN_F32); break; }
 #undef LN_O
 #undef LN_V
+#undef LN_R
   SAMQ_LAUNCH_CHECK("layernorm launch");
   return SAMQ_OK;
 }
@@ -119,7 +146,7 @@ static int ln_launch(const void* x, void* y, const float* gamma, const float* be
 extern "C" int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
                               float eps, int flags, hipStream_t stream) {
   return ln_launch(x, y, gamma, beta, rows, C, eps, (flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32,
-                   (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, stream);
+                   (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, ln_rpw(flags), stream);
 }
 
 extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
@@ -129,5 +156,5 @@ extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, cons
   const int in = (flags & SAMQ_LN_IN_I8) ? LN_I8 : ((flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32);
   const int out = (flags & SAMQ_LN_OUT_I8) ? ((flags & SAMQ_LN_OUT_F32) ? LN_FQ32 : LN_I8)
                                            : ((flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16);
-  return ln_launch(x, y, gamma, beta, rows, C, eps, in, out, in_scale, out_scale, stream);
+  return ln_launch(x, y, gamma, beta, rows, C, eps, in, out, in_scale, out_scale, ln_rpw(flags), stream);
 }

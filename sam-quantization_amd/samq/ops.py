@@ -80,8 +80,10 @@ def w4a16_gemm(a: torch.Tensor, wpacked: torch.Tensor, scales: torch.Tensor, qze
 
 # ----------------------------------------------------------------------------- LayerNorm
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-6,
-              out: Optional[torch.Tensor] = None, out_dtype: torch.dtype = torch.float16) -> torch.Tensor:
-    """Row LayerNorm over the last dim; x f32 or f16 -> f16 (or f32); gamma/beta f32."""
+              out: Optional[torch.Tensor] = None, out_dtype: torch.dtype = torch.float16,
+              rows_per_wave: int = 0) -> torch.Tensor:
+    """Row LayerNorm over the last dim; x f32 or f16 -> f16 (or f32); gamma/beta f32.
+    ``rows_per_wave`` (1, 2, 4; 0 = library default) is a tuning knob (SAMQ_LN_RPW)."""
     _need_cuda(x, gamma, beta)
     c = x.shape[-1]
     assert x.is_contiguous() and x.dtype in (torch.float32, torch.float16)
@@ -90,6 +92,7 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
         out = torch.empty(x.shape, dtype=out_dtype, device=x.device)
     assert out.is_contiguous() and out.dtype in (torch.float16, torch.float32)
     flags = (_lib.LN_IN_F16 if x.dtype == torch.float16 else 0) | (_lib.LN_OUT_F32 if out.dtype == torch.float32 else 0)
+    flags |= rows_per_wave << 16
     rows = x.numel() // c
     _lib.check(_lib.load().samq_layernorm(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), rows, c, float(eps), flags,
                                           _stream()), "layernorm")

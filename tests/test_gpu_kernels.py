@@ -155,18 +155,20 @@ def test_matmul4_rejects_bad_k(cuda):
                        torch.zeros(1, 8, dtype=torch.int32, device=cuda))
 
 
+@pytest.mark.parametrize("rpw", [0, 1, 2, 4])
 @pytest.mark.parametrize("c", [256, 768, 1280])
 @pytest.mark.parametrize("in_dtype", [torch.float32, torch.float16])
-def test_layernorm(cuda, c, in_dtype):
+def test_layernorm(cuda, c, in_dtype, rpw):
+    """1001 rows: ragged against every rows-per-wave grid (4 waves x rpw rows per workgroup)."""
     from samq import ops
     g = torch.Generator().manual_seed(c)
     x = (torch.randn(1001, c, generator=g) * 3 + 1.5).to(in_dtype)
     w = 1 + 0.1 * torch.randn(c, generator=g)
     b = 0.1 * torch.randn(c, generator=g)
     ref = torch.nn.functional.layer_norm(x.float(), (c,), w, b, eps=1e-6).numpy()
-    out = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6)
+    out = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6, rows_per_wave=rpw)
     _close(out, ref, 1.5e-3)
-    out32 = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6, out_dtype=torch.float32)
+    out32 = ops.layernorm(x.to(cuda), w.to(cuda), b.to(cuda), 1e-6, out_dtype=torch.float32, rows_per_wave=rpw)
     _close(out32, ref, 2e-5)
 
 
