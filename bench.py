@@ -242,6 +242,9 @@ def main():
     ap.add_argument("--mode", default="w4a16", choices=("w4a16", "w4a8", "w8a8"))
     ap.add_argument("--groupsize", type=int, default=-1)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="image groups run as concurrent kernel chains on separate HIP streams "
+                         "(0 = 2 when the per-GPU batch is even, else 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -258,6 +261,8 @@ def main():
     model = args.model or ("vit_b" if mode == "w8a8" else "vit_h")
     batch = args.batch or {"w4a16": 4 if world == 1 else 8, "w4a8": 8, "w8a8": 1}[mode]
 
+    if args.lanes <= 0:
+        args.lanes = 2 if batch % 2 == 0 else 1
     t0 = time.time()
     if mode == "w8a8":
         # fq_vit W8A8: random weights calibrated on one seeded image (identical on every rank)
@@ -279,9 +284,9 @@ def main():
     img = torch.randn((batch, 3, 1024, 1024), generator=g, device=dev,
                       dtype=torch.float32 if mode == "w8a8" else torch.float16)
     if args.no_graph:
-        run = lambda: eng(img)  # noqa: E731
+        run = lambda: eng(img, lanes=args.lanes)  # noqa: E731
     else:
-        graph, _ = eng.capture(img)
+        graph, _ = eng.capture(img, lanes=args.lanes)
         run = graph.replay
     for _ in range(args.warmup):
         run()
@@ -319,7 +324,7 @@ def main():
             }[mode] + f", {batch} x 1024x1024 images per GPU", "mode": mode,
                        "model": model, "global_batch": world * batch, "per_gpu_batch": batch,
                        "seq_len": 4096, "parallelism": f"image-parallel x{world} (weights RCCL-broadcast once)",
-                       "graph": not args.no_graph},
+                       "graph": not args.no_graph, "lanes": args.lanes},
             "roofline": roof,
             "e2e": {"tflop_per_image": round(fl["total"] / 1e12, 4), "achieved_tflops_per_gpu": round(e2e_tflops, 1),
                     "frac_of_fp16_peak": round(e2e_tflops / PEAK_FP16_TFLOPS, 4),

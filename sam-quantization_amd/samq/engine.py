@@ -116,8 +116,10 @@ class EncoderEngine:
             return t.to(torch.float16).contiguous()
         return fit(attn.rel_pos_h), fit(attn.rel_pos_w)
 
-    def buffers(self, b: int):
-        bufs = self._bufs.get(b)
+    def buffers(self, b: int, lane: int = 0):
+        """Activation buffers for a batch of ``b`` images; each concurrent lane (``forward``'s
+        ``lanes``) owns its own set."""
+        bufs = self._bufs.get((b, lane))
         if bufs is None:
             g, c, dev = self.grid, self.C, self.device
             hid = self.plans[0].lin1.outfeatures
@@ -134,7 +136,7 @@ class EncoderEngine:
                             att8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
                             hid8=torch.empty((b, g, g, hid), dtype=torch.int8, device=dev))
                 del bufs["xn"], bufs["hid"]
-            self._bufs[b] = bufs
+            self._bufs[(b, lane)] = bufs
         return bufs
 
     # ---------------------------------------------------------------- stages
@@ -188,14 +190,47 @@ class EncoderEngine:
 
     # ---------------------------------------------------------------- forward
     @torch.no_grad()
-    def forward(self, img: torch.Tensor, out_dtype=None) -> torch.Tensor:
+    def forward(self, img: torch.Tensor, out_dtype=None, lanes: int = 1) -> torch.Tensor:
+        """Whole encoder forward.  ``lanes > 1`` splits the batch into that many image groups,
+        each run as its own kernel chain on its own HIP stream (images are independent: per-token
+        LN, per-image attention).  Kernels of one lane fill the CUs another lane leaves idle —
+        the last partial round of GEMM tiles (N=1280: 1.25 rounds of 256 CUs at B=4), and the
+        HBM-bound LayerNorm under the MFMA-bound GEMMs.  Every kernel is batch-invariant, so the
+        result is bit-identical to ``lanes=1`` (tests/test_gpu_encoder.py)."""
         assert img.is_cuda, "EncoderEngine runs on the GPU only"
+        out_dtype = out_dtype or img.dtype
         b = img.shape[0]
-        bufs = self.buffers(b)
+        if lanes <= 1 or b < 2:
+            return self._forward(img, self.buffers(b), out_dtype)
+        lanes = min(lanes, b)
+        assert b % lanes == 0, f"batch {b} does not split into {lanes} lanes"
+        bl = b // lanes
+        cur = torch.cuda.current_stream()
+        streams = self._lane_streams(lanes)
+        for s in streams:
+            s.wait_stream(cur)
+        outs = []
+        for i, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                outs.append(self._forward(img[i * bl:(i + 1) * bl], self.buffers(bl, i), out_dtype))
+        out = torch.empty((b,) + tuple(outs[0].shape[1:]), dtype=out_dtype, device=img.device)
+        for i, s in enumerate(streams):  # nothing was enqueued on ``cur`` since the fork
+            with torch.cuda.stream(s):
+                out[i * bl:(i + 1) * bl].copy_(outs[i])
+            cur.wait_stream(s)
+        return out
+
+    def _lane_streams(self, lanes: int):
+        ss = getattr(self, "_streams", None)
+        if ss is None or len(ss) < lanes:
+            ss = self._streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
+        return ss[:lanes]
+
+    def _forward(self, img: torch.Tensor, bufs, out_dtype) -> torch.Tensor:
         self.embed(img, bufs["x"])
         for p in self.plans:
             self.block(p, bufs)
-        return self.neck(bufs["x"], out_dtype or img.dtype)
+        return self.neck(bufs["x"], out_dtype)
 
     __call__ = forward
 
@@ -208,16 +243,16 @@ class EncoderEngine:
             self.block(p, bufs)
         return bufs["x"].clone()
 
-    def capture(self, img_static: torch.Tensor, out_dtype=None):
+    def capture(self, img_static: torch.Tensor, out_dtype=None, lanes: int = 1):
         """Record one forward on ``img_static`` into a HIP graph; returns ``(graph, out)``;
         ``graph.replay()`` recomputes ``out`` from the current contents of ``img_static``."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self.forward(img_static, out_dtype)
+                self.forward(img_static, out_dtype, lanes)
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            out = self.forward(img_static, out_dtype)
+            out = self.forward(img_static, out_dtype, lanes)
         return graph, out

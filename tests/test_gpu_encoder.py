@@ -77,3 +77,24 @@ def test_batch_and_graph_consistency(cuda, vith32):
     torch.cuda.synchronize()
     assert (out - y2).abs().max().item() == 0.0
     assert torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("lanes", [2, 4])
+def test_lanes_bit_identical(cuda, vith32, lanes):
+    """Image groups on concurrent HIP streams (engine.forward ``lanes``), eager and captured,
+    give exactly the single-chain result: every kernel is batch-invariant."""
+    *_, enc, img, _ = vith32
+    eng = enc.engine()
+    x1 = torch.from_numpy(img).to(cuda)
+    x4 = torch.cat([x1, torch.flip(x1, dims=[-1]), torch.flip(x1, dims=[-2]), -x1])
+    ref = eng(x4, out_dtype=torch.float32)
+    out = eng(x4, out_dtype=torch.float32, lanes=lanes)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    static = x4.clone()
+    graph, gout = eng.capture(static, out_dtype=torch.float32, lanes=lanes)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gout, ref)
+    with pytest.raises(AssertionError):
+        eng(x4[:3], lanes=2)
