@@ -350,7 +350,14 @@ static int i8_cfg_bn(int cfg) {
   switch (cfg) { case 81: case 82: return 256; case 83: return 128; case 84: return 64; default: return 0; }
 }
 
-static int i8_pick_cfg(int M, int N) {
+static int i8_pick_cfg(int M, int N, int bfmt) {
+  // W4 at ViT-H sizes (tools/bench_i8.py, M = 16384 / 32768, profiles/r1_v11_i8_scan.log): the
+  // wide projections (qkv, lin1: N >= 2560) run best on 256x256 tiles, the N=1280 ones (proj,
+  // lin2) on 128x128 tiles (1280 tiles per 16384 rows: 5 even rounds of 256 CUs, not 1.25).
+  if (bfmt == BF_W4 && M >= 8192) {
+    if (N % 256 == 0 && N >= 2560) return 81;
+    if (N % 128 == 0) return 83;
+  }
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);
   if (N % 256 == 0 && t256 >= 512) return 82;
   if (N % 128 == 0 && M >= 256) return 83;
@@ -409,7 +416,7 @@ extern "C" int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const vo
   SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES || (R && ldr % 16 == 0 && ((uintptr_t)R & 15) == 0), SAMQ_ERR_INVALID,
                "i8_gemm: Q8_RES needs a 16-byte aligned residual R with ldr % 16 == 0");
   if (M == 0) return SAMQ_OK;
-  if (cfg <= 0) cfg = i8_pick_cfg(M, N);
+  if (cfg <= 0) cfg = i8_pick_cfg(M, N, bfmt);
   SAMQ_REQUIRE(i8_cfg_bn(cfg) > 0 && N % i8_cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "i8_gemm: N not divisible by tile");
   I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
            I8Epi{a_scale, mid_scale, res_scale, out_scale, R, ldr}};
