@@ -1284,7 +1284,21 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
 // The ping-pong v6 (cfg 57: 256x256 tiles, 4-slot ring, lookahead 3) is 5-7 % faster on the wide
 // projections (qkv N=3840, lin1 N=5120 at M=16384: 1090 / 970 TF/s vs 1016 / 925); with N=1280 its
 // 320 tiles leave a 25 % second round on 256 CUs, where v3's 2-workgroup/CU 128x256 stays ahead.
+// 128x320 tiles (cfg 29) when they make exactly one round on the chip: the N=1280 projections
+// of one 2-image lane (M = 8192: 64 x 4 = 256 tiles) run proj 38 vs 42 us and lin2 105 vs 124 us
+// against cfg 22 (profiles/r1_v12_gemm_scan_m8192.log); at M = 16384 cfg 22 stays ahead.
+static int num_cus() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, c = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    cus = c > 0 ? c : 256;
+  }
+  return cus;
+}
+
 static int pick_cfg(int M, int N, bool grouped) {
+  if (!grouped && N % 320 == 0 && N < 2048 && (int64_t)((M + 127) / 128) * (N / 320) == num_cus()) return 29;
   if (!grouped && N % 256 == 0 && N >= 2048 && M >= 4096) return 57;
   if (N % 256 == 0 && M >= 1024) return 22;
   if (N % 128 == 0 && M >= 512) return 23;
