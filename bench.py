@@ -59,8 +59,9 @@ def pmc_traffic(pattern: str, profile: str):
 
 
 def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
-    """Average duration of every W4A16 GEMM launch of one forward, measured with HIP events on
-    the launch stream; achieved = algorithmic FLOPs (2*M*N*K per launch) / duration."""
+    """Average duration of every W4A16 GEMM launch of one forward at ``bufs_batch`` images per
+    launch (one lane), measured with HIP events on the launch stream, launches back to back
+    (no concurrent lane); achieved = algorithmic FLOPs (2*M*N*K per launch) / duration."""
     from samq import ops
     bufs = eng.buffers(bufs_batch)
     stream = torch.cuda.current_stream()
@@ -87,7 +88,9 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
     for p in eng.plans:
         for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
             alg.append(rows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + rows * lin.outfeatures * out_b)
-    traffic, src = pmc_traffic("w4a16_gemm", "r1_pmc_traffic_w4a16.json") if bufs_batch == 4 else (None, None)
+    # committed PMC passes per GEMM row count: M = 16384 (one B=4 chain), M = 8192 (a 2-image lane)
+    prof = {16384: "r1_pmc_traffic_w4a16.json", 8192: "r1_pmc_traffic_w4a16_m8192.json"}.get(rows)
+    traffic, src = pmc_traffic("w4a16_gemm", prof) if prof else (None, None)
     return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_FP16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_FP16_TFLOPS, 4), traffic=traffic,
                 traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
@@ -306,7 +309,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    roof = {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, batch)
+    # the GEMM launches as the timed step issues them: one lane's images per launch
+    roof = {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, batch // args.lanes)
     fl = flops_per_image(enc)
     total_imgs = world * batch * args.steps
     value = total_imgs / elapsed
