@@ -287,9 +287,9 @@ def main():
     img = torch.randn((batch, 3, 1024, 1024), generator=g, device=dev,
                       dtype=torch.float32 if mode == "w8a8" else torch.float16)
     if args.no_graph:
-        run = lambda: eng(img, lanes=args.lanes)  # noqa: E731
+        run = (lambda: eng(img, lanes=args.lanes)) if args.lanes > 1 else (lambda: eng(img))  # noqa: E731
     else:
-        graph, _ = eng.capture(img, lanes=args.lanes)
+        graph, _ = eng.capture(img, lanes=args.lanes) if args.lanes > 1 else eng.capture(img)
         run = graph.replay
     for _ in range(args.warmup):
         run()
