@@ -359,6 +359,9 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
     if (N % 128 == 0) return 83;
   }
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);
+  // W8 below two rounds of 128x256 tiles (fq_vit vit_b at B=1, M = 4096): 64x64 tiles fill the
+  // chip — per block 77 vs 88-90 us (tools/bench_i8.py --w8-vitb, profiles/r1_v17_w8_scan.log).
+  if (bfmt == BF_W8 && t256 < 512 && N % 64 == 0) return 84;
   if (N % 256 == 0 && t256 >= 512) return 82;
   if (N % 128 == 0 && M >= 256) return 83;
   return 84;

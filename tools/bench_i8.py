@@ -25,7 +25,10 @@ def main():
     ap.add_argument("--m", default="16384,32768")
     ap.add_argument("--cfgs", default="81,82,83")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--w8-vitb", action="store_true", help="W8A8 vit_b shapes (int8 weights, EPI_Q8)")
     args = ap.parse_args()
+    if args.w8_vitb:
+        return w8_vitb(args)
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     cfgs = [int(c) for c in args.cfgs.split(",")]
@@ -67,6 +70,45 @@ def main():
                 print(f"{name:5s} M={m} cfg {c}: {best:8.1f} us  {fl / best / 1e6:7.1f} TOPS "
                       f"({fl / best / 1e6 / 5000 * 100:4.1f}% int8 peak)  identical to cfg 82: {same}", flush=True)
         print(f"M={m} per-block GEMM total: " + "  ".join(f"cfg {c} {t:.1f} us" for c, t in tot.items()), flush=True)
+
+
+def w8_vitb(args):
+    """fq_vit W8A8 vit_b projection shapes (M = 4096 per image), quantising epilogue."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfgs = [int(c) for c in args.cfgs.split(",")]
+    shapes = {"qkv": (768, 2304), "proj": (768, 768), "lin1": (768, 3072), "lin2": (3072, 768)}
+    for m in (int(x) for x in args.m.split(",")):
+        tot = {c: 0.0 for c in cfgs}
+        for name, (k, n) in shapes.items():
+            w = torch.randint(-127, 128, (n, k), device=dev, dtype=torch.int8)
+            packed = ops.w8_repack(w)
+            ws = torch.rand(n, device=dev) * 0.01
+            bias = torch.randn(n, device=dev) * 0.02
+            a = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8)
+
+            def run(c):
+                return ops.w8a8_gemm(a, packed, ws, n, bias, ops.EPI_Q8, 0.02, 0.05) if c == 0 else \
+                    ops.i8_gemm(a, _lib.BF_W8, packed, ws, n, bias, None, ops.EPI_Q8, 0.02, 0.05, cfg=c)
+            ref = run(0)
+            stream = torch.cuda.current_stream()
+            for c in cfgs:
+                same = torch.equal(run(c), ref)
+                best = 1e9
+                for _ in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(args.iters):
+                        run(c)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    best = min(best, e0.elapsed_time(e1) / args.iters * 1e3)
+                tot[c] += best
+                fl = 2.0 * m * n * k
+                print(f"w8 {name:5s} M={m} cfg {c}: {best:7.1f} us  {fl / best / 1e6:7.1f} TOPS  "
+                      f"identical to default pick: {same}", flush=True)
+        print(f"w8 M={m} per-block GEMM total: " + "  ".join(f"cfg {c} {t:.1f} us" for c, t in tot.items()),
+              flush=True)
 
 
 if __name__ == "__main__":
