@@ -63,6 +63,7 @@ class QuantLinear(nn.Module):
         # W4A8: an fq_vit QAct on the input (make_act_quant); None = W4A16
         self.act_quant = None
         self._w4a8 = None
+        self.gemm_cfg = 0   # W4A16 tile config; 0 = the library's per-shape pick (tools/bench_lanes.py)
 
     # -- kernel-side weight layout ------------------------------------------------------
     def prepare(self) -> torch.Tensor:
@@ -105,7 +106,7 @@ class QuantLinear(nn.Module):
     def forward_epilogue(self, x: torch.Tensor, epilogue: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         assert x.shape[-1] == self.qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
         return ops.w4a16_gemm(x, self.prepare(), self.scales, self.qzeros, self.bias, self.outfeatures,
-                              self.groupsize, epilogue, out=out)
+                              self.groupsize, epilogue, out=out, cfg=self.gemm_cfg)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.act_quant is not None:

@@ -52,3 +52,14 @@ for mode in which:
             print(f"{mode} B={batch} lanes={lanes}: {ms:.2f} ms/step  {batch / ms * 1e3:.1f} img/s  "
                   f"eager {ms_eager:.2f} ms  bit-identical to lanes=1: {same}", flush=True)
             del graph
+        if mode == "w4a16":   # lin1 tile A/B inside the 2-lane graph (cfg 22 vs the default pick)
+            for cfg in (22, 0):
+                for p in eng.plans:
+                    p.lin1.gemm_cfg = cfg
+                graph, out = eng.capture(img, lanes=2)
+                ms = step_ms(graph.replay)
+                graph.replay()
+                torch.cuda.synchronize()
+                print(f"{mode} B={batch} lanes=2 lin1 cfg {cfg or 'pick'}: {ms:.2f} ms/step  "
+                      f"bit-identical to lanes=1: {torch.equal(out, base)}", flush=True)
+                del graph
