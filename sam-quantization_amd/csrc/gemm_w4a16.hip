@@ -1299,7 +1299,9 @@ static int num_cus() {
 
 static int pick_cfg(int M, int N, bool grouped) {
   if (!grouped && N % 320 == 0 && N < 2048 && (int64_t)((M + 127) / 128) * (N / 320) == num_cus()) return 29;
-  if (!grouped && N % 256 == 0 && N >= 2048 && M >= 4096) return 57;
+  // v6 from two images up: at M = 4096 (one image) lin1 runs 63.5 us on cfg 22 vs 77.9 on v6 and
+  // qkv is a tie (profiles/r1_v20_gemm_scan_m4096.log)
+  if (!grouped && N % 256 == 0 && N >= 2048 && M >= 8192) return 57;
   if (N % 256 == 0 && M >= 1024) return 22;
   if (N % 128 == 0 && M >= 512) return 23;
   if (N % 64 == 0) return 26;
