@@ -7,23 +7,36 @@ Default (the headline, BASELINE config 3/4): ``--mode w4a16`` = ViT-H GPTQ int4 
 activations.  ``--mode w4a8`` (config 5): ViT-H int4 weights x int8 activations on the int8 MFMA,
 batch 8.  ``--mode w8a8`` (config 2): vit_b fq_vit W8A8, batch 1.
 
-One process per GPU (for N > 1 launched by ``torch.distributed.run``; RANK / LOCAL_RANK /
-WORLD_SIZE / MASTER_* from the env).  A "step" = one encoder forward over the per-GPU batch of
-synthetic images already resident in HBM (a HIP-graph replay of the fused engine).  Weights are
-random-init ViT-H, RTN-quantised into the reference's packed int4 format on rank 0 and RCCL-
-broadcast to the other ranks (the only collective on the data path).  Per-GPU work is fixed
-("weak" scaling): batch 4 per GPU at N=1 (BASELINE config 3), 8 per GPU at N>1 (config 4 at
-N=8 = global batch 64).
+One process per GPU.  Under ``torch.distributed.run`` (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_* in the env) every process is one rank.  Started bare with ``--gpus N > 1`` the script
+launches its own N ranks: it starts ``torch.distributed.run`` as a CHILD process before anything
+touches the GPU, relays rank 0's line and exits with the child's status (the reference's
+``mp.spawn`` + ``init_process_group`` pattern, train_sm.py:587-590, 630-636, without re-exec).
+A "step" = one encoder forward over the per-GPU batch of synthetic images already resident in
+HBM (a HIP-graph replay of the fused engine).  Weights are random-init ViT-H, RTN-quantised into
+the reference's packed int4 format on rank 0 and RCCL-broadcast to the other ranks (the only
+collective on the data path).  One seeded global batch (image i drawn from seed 1234 + i) is
+sharded contiguously over the ranks (``samq.dist.shard``); per-GPU work is fixed ("weak"
+scaling): 4 images per GPU at N=1 (BASELINE config 3), 8 per GPU at N>1 (config 4 at N=8 =
+global batch 64).
 
 Besides the throughput line, it reports for the dominant kernel (all W4A16 GEMM launches of one
-forward) its live roofline fraction from HIP events on the launch stream, and the CPU baseline:
-the oracle restatement of the reference's fp32 CPU fake-quant path on one image (rank 0, N=1).
+forward) its roofline fraction measured INSIDE the timed configuration (HIP events captured into
+the same HIP graph as external event nodes, on each lane's stream; see ``step_profile``), the
+isolated-launch figure next to it, and the CPU baseline: the oracle restatement of the
+reference's fp32 CPU fake-quant path (median of 3 one-image runs after one warm-up, rank 0, N=1).
+
+``--dry-run --backend gloo`` exercises the launcher / sharding / weight broadcast on the CPU
+(tiny model, no GPU) for the multi-process tests.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -59,9 +72,10 @@ def pmc_traffic(pattern: str, profile: str):
 
 
 def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
-    """Average duration of every W4A16 GEMM launch of one forward at ``bufs_batch`` images per
-    launch (one lane), measured with HIP events on the launch stream, launches back to back
-    (no concurrent lane); achieved = algorithmic FLOPs (2*M*N*K per launch) / duration."""
+    """ISOLATED figure: average duration of every W4A16 GEMM launch of one forward at
+    ``bufs_batch`` images per launch (one lane), HIP events on the launch stream, launches back to
+    back with no concurrent lane; achieved = algorithmic FLOPs (2*M*N*K per launch) / duration.
+    The headline ``roofline`` comes from ``step_profile`` (inside the timed graph)."""
     from samq import ops
     bufs = eng.buffers(bufs_batch)
     stream = torch.cuda.current_stream()
@@ -101,6 +115,43 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
 
 
 PEAK_INT8_TOPS = 5000.0     # MI355X dense int8 MFMA (2x fp16, MI355X_MICROARCH.md)
+
+# committed rocprofv3 --kernel-trace --stats summaries of the timed configuration itself, one per
+# kernel-source build: `tools/instep_profile.sh` runs `rocprofv3 --kernel-trace --stats -- python3
+# bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-isolated` (every GEMM dispatch in it is a
+# graph replay or capture warm-up with the timed lanes) and commits the kernel stats as
+# profiles/instep_<mode>_b<images per launch>_l<lanes>_<source hash>.csv
+
+
+def source_hash() -> str:
+    """sha1 of the HIP sources + build recipe the library is compiled from (12 hex digits)."""
+    import hashlib
+    h = hashlib.sha1()
+    pkg = REPO / "sam-quantization_amd"
+    for f in sorted(list((pkg / "csrc").glob("*")) + [pkg / "Makefile", REPO / "include" / "samq.h"]):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:12]
+
+
+def in_step_from_profile(mode, imgs_per_launch, lanes, flops_launch, peak):
+    """GEMM roofline of the timed replays (concurrent lanes included) from the committed rocprof
+    kernel stats: average algorithmic FLOPs per launch / average GEMM dispatch duration."""
+    name = f"instep_{mode}_b{imgs_per_launch}_l{lanes}_{source_hash()}.csv"
+    f = REPO / "profiles" / name
+    if not f.exists() or not flops_launch:
+        return None
+    import csv
+    tot_ns = n = 0
+    for r in csv.DictReader(open(f)):
+        if "w4a16_gemm" in r["Name"]:
+            tot_ns += float(r["TotalDurationNs"])
+            n += int(r["Calls"])
+    if not n:
+        return None
+    ach = flops_launch / (tot_ns / n * 1e-9) / 1e12
+    return dict(achieved=round(ach, 1), frac=round(ach / peak, 4), avg_launch_us=round(tot_ns / n / 1e3, 2),
+                dispatches=n, source=f"profiles/{name}")
 
 
 def _time_launches(launches, reps=3):
@@ -195,12 +246,16 @@ def cpu_baseline(model_name: str, mode: str = "w4a16"):
         o = sam_ref.EncoderOracle(cfg, st)
         what = "fp32 CPU fake-quant op graph (oracle/sam_ref.py)"
     img = torch.randn(1, 3, 1024, 1024, generator=g)
-    t0 = time.perf_counter()
-    o(img)
-    dt = time.perf_counter() - t0
+    o(img)   # warm-up (allocator, thread pool)
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        o(img)
+        runs.append(time.perf_counter() - t0)
+    dt = statistics.median(runs)
     return dict(value=round(1.0 / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample=f"1 image, {model_name} {what}, "
-                       f"{dt:.1f} s wall, torch {threads} threads, CPU: {_cpu_model()}")
+                sample=f"1 image, {model_name} {what}; median of 3 runs after 1 warm-up "
+                       f"({', '.join(f'{r:.2f}' for r in runs)} s), torch {threads} threads, CPU: {_cpu_model()}")
 
 
 def _state_shapes(cfg):
@@ -235,6 +290,67 @@ def _cpu_model():
     return "unknown"
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """``--gpus N`` without a torchrun environment: start N fresh rank processes through
+    ``torch.distributed.run`` as a child (nothing in this process has touched the GPU), let rank 0
+    print the JSON line on the inherited stdout, and return the child's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), str(Path(__file__).resolve()), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    log(f"launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def local_images(start: int, stop: int, dev, dtype, size: int = 1024) -> torch.Tensor:
+    """Images [start, stop) of the seeded global batch: image i ~ N(0, 1) from seed 1234 + i, so
+    every sharding of the global batch sees the same pixels."""
+    out = torch.empty((stop - start, 3, size, size), dtype=dtype, device=dev)
+    for j, i in enumerate(range(start, stop)):
+        g = torch.Generator(device=dev).manual_seed(1234 + i)
+        out[j] = torch.randn((3, size, size), generator=g, device=dev, dtype=torch.float32).to(dtype)
+    return out
+
+
+def dry_run(args, rank: int, world: int) -> None:
+    """CPU rehearsal of the multi-rank path (gloo): shard the seeded global batch, broadcast a
+    tiny quantised encoder from rank 0, gather per-rank shard / checksum records on rank 0."""
+    from samq import dist as sdist
+    from samq.synthetic import random_quant_encoder
+    per_gpu = args.batch or 8
+    gb = per_gpu * world
+    start, stop = sdist.shard(gb, rank, world)
+    imgs = local_images(start, stop, torch.device("cpu"), torch.float32, size=32)
+    enc = random_quant_encoder("vit_b", -1, device="cpu", depth=1, img_size=64, init=(rank == 0))
+    t0 = time.perf_counter()
+    nbytes = sdist.broadcast_state(enc, src=0)
+    t_bc = time.perf_counter() - t0
+    wsum = float(sum(t.double().sum() for t in enc.state_dict().values() if torch.is_tensor(t)))
+    rec = dict(rank=rank, shard=[start, stop], image_checksums=[float(x.double().sum()) for x in imgs],
+               state_checksum=wsum, broadcast_bytes=nbytes, broadcast_s=round(t_bc, 4))
+    on = dist.is_initialized()
+    recs = [None] * world
+    if on:
+        dist.all_gather_object(recs, rec)
+    else:
+        recs = [rec]
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "img/s", "n_gpus": world, "dry_run": True,
+                          "backend": dist.get_backend() if on else None,
+                          "world_size_seen": dist.get_world_size() if on else 1,
+                          "global_batch": gb, "per_gpu_batch": per_gpu, "ranks": recs}), flush=True)
+    if on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,33 +363,54 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--lanes", type=int, default=0,
                     help="image groups run as concurrent kernel chains on separate HIP streams "
-                         "(0 = 2 when the per-GPU batch is even, else 1)")
+                         "(0 = 2 when the per-GPU batch is even, else 1; W8A8 runs one chain)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the live roofline passes (for a rocprof trace of the timed replays only)")
+    ap.add_argument("--backend", default="", help="torch.distributed backend (default nccl = RCCL; gloo for --dry-run)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU rehearsal of the multi-rank path (no GPU)")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
 
-    import samq
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+
     from samq import dist as sdist
-    from samq.synthetic import flops_per_image, random_fq_encoder, random_quant_encoder
-
-    rank, world = sdist.init_from_env()
+    rank, world = sdist.init_from_env(args.backend or ("gloo" if args.dry_run else None))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    if args.dry_run:
+        return dry_run(args, rank, world)
+
+    import samq
+    from samq.synthetic import flops_per_image, random_fq_encoder, random_quant_encoder
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(dev)
     mode = args.mode
     model = args.model or ("vit_b" if mode == "w8a8" else "vit_h")
     batch = args.batch or {"w4a16": 4 if world == 1 else 8, "w4a8": 8, "w8a8": 1}[mode]
-
-    if args.lanes <= 0:
+    if mode == "w8a8":
+        if args.lanes > 1:
+            ap.error("--mode w8a8 runs one kernel chain (W8A8Engine has no lanes)")
+        args.lanes = 1
+    elif args.lanes <= 0:
         args.lanes = 2 if batch % 2 == 0 else 1
+    if batch % args.lanes:
+        ap.error(f"--lanes {args.lanes} does not divide the per-GPU batch {batch}")
+
     t0 = time.time()
+    t_bc = 0.0
     if mode == "w8a8":
         # fq_vit W8A8: random weights calibrated on one seeded image (identical on every rank)
         enc = random_fq_encoder(model, device=dev)
         nbytes = 0
     else:
         enc = random_quant_encoder(model, args.groupsize, device=dev, init=(rank == 0))
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
         nbytes = sdist.broadcast_state(enc, src=0)
+        torch.cuda.synchronize()
+        t_bc = time.perf_counter() - tb
         if mode == "w4a8":
             enc.half()
             samq.make_act_quant(enc)
@@ -281,16 +418,20 @@ def main():
             cal = torch.randn((1, 3, 1024, 1024), generator=gcal).to(dev, torch.float16)
             samq.calibrate_act_quant(enc, enc.module_forward, [cal])
     eng = enc.engine()
-    log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB)")
+    log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB "
+        f"in {t_bc * 1e3:.1f} ms)")
 
-    g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    img = torch.randn((batch, 3, 1024, 1024), generator=g, device=dev,
-                      dtype=torch.float32 if mode == "w8a8" else torch.float16)
-    if args.no_graph:
-        run = (lambda: eng(img, lanes=args.lanes)) if args.lanes > 1 else (lambda: eng(img))  # noqa: E731
-    else:
+    gb = world * batch
+    start, stop = sdist.shard(gb, rank, world)
+    img = local_images(start, stop, dev, torch.float32 if mode == "w8a8" else torch.float16)
+
+    def make_run():
+        if args.no_graph:
+            return (lambda: eng(img, lanes=args.lanes)) if args.lanes > 1 else (lambda: eng(img))  # noqa: E731
         graph, _ = eng.capture(img, lanes=args.lanes) if args.lanes > 1 else eng.capture(img)
-        run = graph.replay
+        return graph.replay
+
+    run = make_run()
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
@@ -309,10 +450,46 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    # the GEMM launches as the timed step issues them: one lane's images per launch
-    roof = {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, batch // args.lanes)
+    c = enc.pos_embed.shape[-1]
+    rows = stop - start
+    per_launch_imgs = rows // args.lanes
+    peak = PEAK_FP16_TFLOPS if mode == "w4a16" else PEAK_INT8_TOPS
+    # (1) live, isolated: every GEMM launch of one forward at the lane's size, HIP events on the
+    # launch stream, back to back (the headline `achieved` / `frac`)
+    skip = args.no_isolated
+    iso = (dict(achieved=None, frac=None, avg_launch_us=None, launches_timed=0) if skip else
+           {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, per_launch_imgs))
+    if mode == "w4a16":
+        alg = []
+        trows = per_launch_imgs * 4096
+        for p in eng.plans:
+            for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
+                alg.append(trows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + trows * lin.outfeatures * out_b)
+        profile = {16384: "r1_pmc_traffic_w4a16.json", 8192: "r1_pmc_traffic_w4a16_m8192.json"}.get(trows)
+        traffic, src = pmc_traffic("w4a16_gemm", profile) if profile else (None, None)
+        kernel = "w4a16_gemm_pp2 (qkv, lin1) + w4a16_gemm_v3 (proj, lin2): all 4 ViT-H projection shapes"
+        alg_b = round(sum(alg) / len(alg))
+        flops_launch = sum(2.0 * trows * lin.infeatures * lin.outfeatures
+                           for lin in (eng.plans[0].qkv, eng.plans[0].proj, eng.plans[0].lin1, eng.plans[0].lin2)) / 4
+    else:
+        traffic, src, alg_b, flops_launch = None, None, None, None
+        kernel = ("i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)" if mode == "w4a8"
+                  else "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)")
+    live = dict(achieved=iso["achieved"], frac=iso["frac"], avg_launch_us=iso["avg_launch_us"],
+                launches_timed=iso["launches_timed"],
+                method="HIP events on the launch stream around every GEMM launch of one forward at the lane's "
+                       "size, back to back with no concurrent lane (3 reps)")
+    ins = in_step_from_profile(mode, per_launch_imgs, args.lanes, flops_launch, peak)
+    head = ins if ins else live
+    roof = dict(bound="mfma", achieved=head["achieved"], peak=peak, unit="TFLOP/s", frac=head["frac"],
+                traffic=traffic, traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
+                algorithmic_bytes_per_launch=alg_b, kernel=kernel, avg_launch_us=head["avg_launch_us"],
+                images_per_launch=per_launch_imgs,
+                source=("in-step: the committed rocprofv3 kernel stats of this command on this build "
+                        f"({ins['source']})" if ins else "live isolated (no committed in-step profile for this build)"),
+                in_step=ins, isolated=live)
     fl = flops_per_image(enc)
-    total_imgs = world * batch * args.steps
+    total_imgs = gb * args.steps
     value = total_imgs / elapsed
     if rank == 0:
         e2e_tflops = value / world * fl["total"] / 1e12
@@ -326,13 +503,16 @@ def main():
                 "w4a8": f"SAM {model} image encoder W4A8 (GPTQ int4 weights, int8 minmax activations)",
                 "w8a8": f"SAM {model} image encoder W8A8 fq_vit (int8 per-channel weights, int8 activations)",
             }[mode] + f", {batch} x 1024x1024 images per GPU", "mode": mode,
-                       "model": model, "global_batch": world * batch, "per_gpu_batch": batch,
+                       "model": model, "global_batch": gb, "per_gpu_batch": batch,
                        "seq_len": 4096, "parallelism": f"image-parallel x{world} (weights RCCL-broadcast once)",
                        "graph": not args.no_graph, "lanes": args.lanes},
             "roofline": roof,
             "e2e": {"tflop_per_image": round(fl["total"] / 1e12, 4), "achieved_tflops_per_gpu": round(e2e_tflops, 1),
                     "frac_of_fp16_peak": round(e2e_tflops / PEAK_FP16_TFLOPS, 4),
                     "frac_of_int8_peak": round(e2e_tflops / (2 * PEAK_FP16_TFLOPS), 4)},
+            "dist": {"backend": dist.get_backend() if world > 1 else None, "world_size_seen": world,
+                     "broadcast_bytes": nbytes, "broadcast_ms": round(t_bc * 1e3, 2),
+                     "rank0_shard": [start, stop]},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(model, mode)

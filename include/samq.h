@@ -60,8 +60,10 @@ size_t samq_w4_packed_words(int K, int N);
  * by load_quant (replaces the reference's per-call B-tile addressing, quant_linear.py:292-294). */
 int samq_w4_repack(const int32_t* qweight, int32_t* packed, int K, int N, hipStream_t stream);
 
-/* Same with an explicit fragment layout (1: 32x32x16 MFMA order, 2: 16x16x32 order); for the
- * tuning entry point samq_w4a16_gemm_cfg (cfg >= 40 expects layout 2, others layout 1). */
+/* Same with an explicit fragment layout: 1 = the W4A16 layout (32x32x16 MFMA order, what
+ * samq_w4_repack produces and every samq_w4a16_gemm_cfg config of this library consumes),
+ * 3 = the W4A8 layout (samq_w4a8_gemm / samq_i8_gemm_cfg).  Layout 2 exists only in the
+ * tuning build (make tuning); this library rejects it with SAMQ_ERR_INVALID. */
 int samq_w4_repack_layout(const int32_t* qweight, int32_t* packed, int K, int N, int layout,
                           hipStream_t stream);
 
@@ -75,8 +77,15 @@ int samq_w4a16_gemm(const void* A, int64_t lda, const int32_t* wpacked, const vo
                     const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N,
                     int K, int groupsize, int epilogue, hipStream_t stream);
 
-/* Same with an explicit tile configuration (0 = automatic); for tuning and tests.
- * 1: 256x256 (8 waves)  2: 256x128  3: 128x128  4: 64x64  5: 64x32  6: 128x256. */
+/* Same with an explicit tile configuration (0 = automatic); for tests and in-graph A/B runs.
+ * All accept layout-1 weights and compute the same result (up to fp32 summation order):
+ *   1 256x256  2 256x128  3 128x128  4 64x64  5 64x32  6 128x256 (1 wave row)  7 256x256
+ *   (8 waves in N)  9 128x256                               -- v1, register-staged
+ *   21 256x256  22 128x256  23 128x128  24 256x128  25 128x256  26 64x64
+ *   29 128x320  30 256x320  31 128x320                      -- v3, LDS-DMA ring
+ *   55 56 57 58 62 64 65 (groupsize == K only)             -- v6 ping-pong, 256x256
+ * Any other value (the tuning build's timing-only and layout-2 configs) returns
+ * SAMQ_ERR_INVALID. */
 int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
                         const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M,
                         int N, int K, int groupsize, int epilogue, int cfg, hipStream_t stream);

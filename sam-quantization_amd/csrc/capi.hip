@@ -23,3 +23,4 @@ int check_hip(hipError_t e, const char* what) {
 extern "C" const char* samq_last_error(void) { return samq::g_last_error.c_str(); }
 
 extern "C" int samq_version(void) { return 100; }
+

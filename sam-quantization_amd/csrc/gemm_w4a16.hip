@@ -1223,11 +1223,14 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 56: return launch_pp2<2, 4, 2, 2, 4, 2, EPI>(a, st);   // 4 slots, lookahead 2 (DMA in both phases)
       case 57: return launch_pp2<2, 4, 2, 2, 4, 3, EPI>(a, st);   // 4 slots, lookahead 3
       case 58: return launch_pp2<2, 4, 2, 1, 4, 2, EPI>(a, st);   // 1 phase / K tile, 4 slots, lookahead 2
-      case 60: return launch_pp2<1, 8, 1, 2, 4, 3, EPI>(a, st);   // 1x8 waves (256x32 each): B unpacked once
-      case 61: return launch_pp2<1, 8, 1, 4, 4, 3, EPI>(a, st);   // 1x8 waves, 4 k-phases
       case 62: return launch_pp2<4, 2, 4, 2, 4, 3, EPI>(a, st);   // 4x2 waves (64x128 each): A read 2x, B 4x
       case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16>(a, st);  // cfg 57 on 16x16x32 MFMA
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
+#ifdef SAMQ_TUNING
+      // tuning build only (make tuning): untested shapes and TIMING-ONLY variants that compute
+      // wrong results on purpose -- never reachable through the product library
+      case 60: return launch_pp2<1, 8, 1, 2, 4, 3, EPI>(a, st);   // 1x8 waves (256x32 each): B unpacked once
+      case 61: return launch_pp2<1, 8, 1, 4, 4, 3, EPI>(a, st);   // 1x8 waves, 4 k-phases
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1242,6 +1245,7 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
                 h[0] / n, h[1] / n, h[2] / n, h[3] / n);
         return r;
       }
+#endif
       default: break;
     }
   }
@@ -1252,18 +1256,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
     case 24: return launch_v3<256, 128, 2, 2, EPI, GR>(a, st);
     case 25: return launch_v3<128, 256, 1, 4, EPI, GR>(a, st);
     case 26: return launch_v3<64, 64, 2, 2, EPI, GR>(a, st);
-    case 27: return launch_v3<128, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
-    case 28: return launch_v3<256, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
     // 320-column tiles: ViT-H N in {1280, 3840, 5120} and M = 128*B give whole waves of tiles
     case 29: return launch_v3<128, 320, 2, 5, EPI, GR>(a, st);
     case 30: return launch_v3<256, 320, 2, 5, EPI, GR>(a, st);
     case 31: return launch_v3<128, 320, 1, 5, EPI, GR>(a, st);
-    // v4 (16x16x32, packed LAYOUT 2)
-    case 41: return launch_v4<128, 256, 2, 4, EPI, GR>(a, st);
-    case 42: return launch_v4<256, 256, 2, 4, EPI, GR>(a, st);
-    case 43: return launch_v4<128, 128, 2, 2, EPI, GR>(a, st);
-    case 44: return launch_v4<64, 64, 2, 2, EPI, GR>(a, st);
-    case 45: return launch_v4<128, 256, 4, 2, EPI, GR>(a, st);
     case 1: return launch_cfg<256, 256, 2, 4, EPI, GR>(a, st);
     case 2: return launch_cfg<256, 128, 2, 2, EPI, GR>(a, st);
     case 3: return launch_cfg<128, 128, 2, 2, EPI, GR>(a, st);
@@ -1271,9 +1267,19 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
     case 5: return launch_cfg<64, 32, 2, 1, EPI, GR>(a, st);
     case 6: return launch_cfg<128, 256, 1, 4, EPI, GR>(a, st);
     case 7: return launch_cfg<256, 256, 1, 8, EPI, GR>(a, st);
-    case 8: return launch_cfg<256, 128, 1, 4, EPI, GR>(a, st);
     case 9: return launch_cfg<128, 256, 2, 4, EPI, GR>(a, st);
+#ifdef SAMQ_TUNING
+    case 8: return launch_cfg<256, 128, 1, 4, EPI, GR>(a, st);
     case 11: return launch_cfg<256, 256, 2, 4, EPI, GR, 0>(a, st);   // literal-constant unpack (A/B)
+    case 27: return launch_v3<128, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
+    case 28: return launch_v3<256, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
+    // v4 (16x16x32): needs weights repacked in LAYOUT 2 -- the caller's responsibility here
+    case 41: return launch_v4<128, 256, 2, 4, EPI, GR>(a, st);
+    case 42: return launch_v4<256, 256, 2, 4, EPI, GR>(a, st);
+    case 43: return launch_v4<128, 128, 2, 2, EPI, GR>(a, st);
+    case 44: return launch_v4<64, 64, 2, 2, EPI, GR>(a, st);
+    case 45: return launch_v4<128, 256, 4, 2, EPI, GR>(a, st);
+#endif
     default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown tile config");
   }
 }
@@ -1333,7 +1339,12 @@ extern "C" int samq_w4_repack_layout(const int32_t* qweight, int32_t* packed, in
   SAMQ_REQUIRE(qweight && packed, SAMQ_ERR_INVALID, "w4_repack: null pointer");
   SAMQ_REQUIRE(K > 0 && N > 0 && K % 64 == 0, SAMQ_ERR_INVALID, "w4_repack: K must be a positive multiple of 64");
   SAMQ_REQUIRE(N % 32 == 0, SAMQ_ERR_INVALID, "w4_repack: N must be a multiple of 32");
+#ifdef SAMQ_TUNING
   SAMQ_REQUIRE(layout >= 1 && layout <= 3, SAMQ_ERR_INVALID, "w4_repack: layout must be 1, 2 or 3");
+#else
+  // layout 2 feeds only the tuning-build v4 kernels; the product library never consumes it
+  SAMQ_REQUIRE(layout == 1 || layout == 3, SAMQ_ERR_INVALID, "w4_repack: layout must be 1 or 3");
+#endif
   SAMQ_REQUIRE(layout != 3 || K % 128 == 0, SAMQ_ERR_INVALID, "w4_repack: layout 3 needs K % 128 == 0");
   const int64_t total = (int64_t)K * N / 8;
   const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);

@@ -10,7 +10,9 @@ import ctypes
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libsamq_hip.so"
+# SAMQ_LIB=tuning selects the tuning build (make tuning: adds timing-only tile configs); tools only
+LIB_PATH = Path(__file__).resolve().parent / (
+    "libsamq_hip_tuning.so" if os.environ.get("SAMQ_LIB") == "tuning" else "libsamq_hip.so")
 
 SAMQ_OK = 0
 SAMQ_ERR_INVALID = -1

@@ -17,12 +17,14 @@ The residual stream ``x`` stays fp32 in HBM (precision: SURVEY.md §7 "Hard part
 Patch embedding (+bias +pos_embed) and the neck convolutions are implicit-GEMM HIP kernels
 (``csrc/conv_gemm.hip``: patches gathered from the NCHW image, 3x3 taps from the NHWC map, no
 im2col copies) plus the HIP LayerNorm; the only torch op left is the final NHWC -> NCHW view
-change of the output.  W4A8 keeps its patch embedding in fp32 (a vendor fp32 GEMM): its first
-int8 quantiser sits right behind it.
+change of the output.  W4A8 keeps its patch embedding in fp32 (``samq_patch_embed_f32``, the
+fp32-MFMA twin of the implicit GEMM): its first int8 quantiser sits right behind it.
 All activation buffers are allocated once per batch size and reused; ``capture()`` records the
 whole forward into a HIP graph for launch-overhead-free replay.
 """
 from __future__ import annotations
+
+from collections import OrderedDict
 
 import torch
 import torch.nn.functional as F
@@ -80,6 +82,9 @@ class EncoderEngine:
         pe = enc.patch_embed.proj
         self.patch = pe.kernel_size[0]
         self.pe_w = pe.weight.detach().reshape(pe.weight.shape[0], -1).to(torch.float16).contiguous()
+        # W4A8 embeds in fp32: the f32 weight copy is made here, on the construction stream,
+        # before any lane fork (a lazy copy on lane 0's stream would race lane 1's first read)
+        self.pe_w32 = self.pe_w.float().contiguous() if self.w4a8 else None
         self.pe_b = pe.bias.detach().float().contiguous() if pe.bias is not None else None
         self.pos = enc.pos_embed.detach().float().contiguous() if enc.pos_embed is not None else None
         n0, n1, n2, n3 = enc.neck
@@ -90,7 +95,8 @@ class EncoderEngine:
         self.n2_w_tap = n2.weight.detach().permute(0, 2, 3, 1).to(torch.float16).contiguous()
         self.n3 = (n3.weight.detach().float().contiguous(), n3.bias.detach().float().contiguous(), float(n3.eps))
         self.out_chans = n0.weight.shape[0]
-        self._bufs = {}
+        self._bufs = OrderedDict()   # (images, lane) -> activation buffers, most recent last
+        self.max_cached_batches = 2  # distinct per-lane batch sizes kept (captured graphs pin their own)
         self._key = self._make_key(enc)
 
     # ---------------------------------------------------------------- helpers
@@ -120,7 +126,14 @@ class EncoderEngine:
         """Activation buffers for a batch of ``b`` images; each concurrent lane (``forward``'s
         ``lanes``) owns its own set."""
         bufs = self._bufs.get((b, lane))
-        if bufs is None:
+        if bufs is not None:
+            self._bufs.move_to_end((b, lane))
+        else:
+            sizes = list(OrderedDict.fromkeys(k[0] for k in self._bufs))
+            while len(sizes) >= self.max_cached_batches and sizes[0] != b:
+                old = sizes.pop(0)   # evict the least recently used batch size (all its lanes)
+                for k in [k for k in self._bufs if k[0] == old]:
+                    del self._bufs[k]
             g, c, dev = self.grid, self.C, self.device
             hid = self.plans[0].lin1.outfeatures
             assert all(p.lin1.outfeatures == hid for p in self.plans)
@@ -139,6 +152,10 @@ class EncoderEngine:
             self._bufs[(b, lane)] = bufs
         return bufs
 
+    def release(self) -> None:
+        """Drop every cached activation buffer (graphs from ``capture`` keep their own alive)."""
+        self._bufs.clear()
+
     # ---------------------------------------------------------------- stages
     def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
         """Patch embedding + bias + pos_embed into the fp32 residual stream: one implicit-GEMM HIP
@@ -149,8 +166,6 @@ class EncoderEngine:
         if not self.w4a8:
             ops.patch_embed(img.to(torch.float16).contiguous(), self.pe_w, self.pe_b, pos, p, out=x32)
             return
-        if getattr(self, "pe_w32", None) is None:
-            self.pe_w32 = self.pe_w.float().contiguous()
         ops.patch_embed(img.to(torch.float32).contiguous(), self.pe_w32, self.pe_b, pos, p, out=x32)
 
     def block_w4a8(self, p: _BlockPlan, bufs) -> None:
@@ -196,14 +211,18 @@ class EncoderEngine:
         LN, per-image attention).  Kernels of one lane fill the CUs another lane leaves idle —
         the last partial round of GEMM tiles (N=1280: 1.25 rounds of 256 CUs at B=4), and the
         HBM-bound LayerNorm under the MFMA-bound GEMMs.  Every kernel is batch-invariant, so the
-        result is bit-identical to ``lanes=1`` (tests/test_gpu_encoder.py)."""
+        result is bit-identical to ``lanes=1`` (tests/test_gpu_encoder.py).
+
+        Returns ``(B, out_chans, H, W)`` in channels-last memory (an NCHW view of the engine's
+        NHWC tokens) for every ``lanes``; ``lanes`` must divide the batch (``ValueError``)."""
         assert img.is_cuda, "EncoderEngine runs on the GPU only"
         out_dtype = out_dtype or img.dtype
         b = img.shape[0]
         if lanes <= 1 or b < 2:
             return self._forward(img, self.buffers(b), out_dtype)
         lanes = min(lanes, b)
-        assert b % lanes == 0, f"batch {b} does not split into {lanes} lanes"
+        if b % lanes:
+            raise ValueError(f"batch {b} does not split into {lanes} lanes")
         bl = b // lanes
         cur = torch.cuda.current_stream()
         streams = self._lane_streams(lanes)
@@ -213,7 +232,8 @@ class EncoderEngine:
         for i, s in enumerate(streams):
             with torch.cuda.stream(s):
                 outs.append(self._forward(img[i * bl:(i + 1) * bl], self.buffers(bl, i), out_dtype))
-        out = torch.empty((b,) + tuple(outs[0].shape[1:]), dtype=out_dtype, device=img.device)
+        n, c, h, w = outs[0].shape
+        out = torch.empty((b, h, w, c), dtype=out_dtype, device=img.device).permute(0, 3, 1, 2)
         for i, s in enumerate(streams):  # nothing was enqueued on ``cur`` since the fork
             with torch.cuda.stream(s):
                 out[i * bl:(i + 1) * bl].copy_(outs[i])
@@ -255,4 +275,8 @@ class EncoderEngine:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             out = self.forward(img_static, out_dtype, lanes)
+        # the graph replays into these buffers: keep them alive with it, whatever the cache evicts
+        b = img_static.shape[0]
+        nl = min(lanes, b) if lanes > 1 and b >= 2 else 1
+        graph.samq_buffers = [self._bufs[(b // nl, i)] for i in range(nl)]
         return graph, out

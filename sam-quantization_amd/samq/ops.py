@@ -18,6 +18,9 @@ EPI_F32 = _lib.EPI_F32
 EPI_Q8 = _lib.EPI_Q8
 EPI_Q8_GELU = _lib.EPI_Q8_GELU
 EPI_Q8_RES = _lib.EPI_Q8_RES
+
+# W4A16 tile configs of the product library (include/samq.h, samq_w4a16_gemm_cfg); 0 = automatic
+W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65))
 _Q8_EPIS = (EPI_Q8, EPI_Q8_GELU, EPI_Q8_RES)
 
 
@@ -325,3 +328,4 @@ def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_po
         heads, c // heads, window, float(sm_scale), float(s_qkv), float(s_a1), float(s_a2), float(s_out), _stream()),
         "rel_attention_q8")
     return out
+

@@ -65,6 +65,17 @@ class QuantLinear(nn.Module):
         self._w4a8 = None
         self.gemm_cfg = 0   # W4A16 tile config; 0 = the library's per-shape pick (tools/bench_lanes.py)
 
+    @property
+    def gemm_cfg(self) -> int:
+        return self._gemm_cfg
+
+    @gemm_cfg.setter
+    def gemm_cfg(self, cfg: int) -> None:
+        cfg = int(cfg)
+        if cfg != 0 and cfg not in ops.W4A16_CFGS:
+            raise ValueError(f"gemm_cfg {cfg} is not a product tile config (0 or one of {sorted(ops.W4A16_CFGS)})")
+        self._gemm_cfg = cfg
+
     # -- kernel-side weight layout ------------------------------------------------------
     def prepare(self) -> torch.Tensor:
         """Repack ``qweight`` for the kernel (once; redone if the buffer was replaced)."""

@@ -66,3 +66,33 @@ def test_shard_covers_everything():
             parts = [shard(n, r, w) for r in range(w)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+
+
+def test_bench_launches_its_own_ranks_and_shards_the_global_batch():
+    """``bench.py --gpus 2`` started bare (no torchrun env) spawns its 2 ranks as a child
+    ``torch.distributed.run`` and relays ONE line from rank 0; the seeded global batch is split
+    contiguously and each rank's images are exactly the single-process images of those indices;
+    the packed weights reach rank 1 through the broadcast (gloo here, RCCL on the GPU box)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--backend", "gloo", "--dry-run",
+                        "--batch", "3"], capture_output=True, text=True, timeout=300, env=env, cwd=str(repo))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["world_size_seen"] == 2 and out["backend"] == "gloo"
+    assert out["global_batch"] == 6
+    ranks = sorted(out["ranks"], key=lambda d: d["rank"])
+    assert [d["shard"] for d in ranks] == [[0, 3], [3, 6]]
+    assert ranks[0]["state_checksum"] == ranks[1]["state_checksum"]
+    assert ranks[1]["broadcast_bytes"] > 0
+    sys.path.insert(0, str(repo))
+    import bench
+    ref = bench.local_images(0, 6, torch.device("cpu"), torch.float32, size=32)
+    got = ranks[0]["image_checksums"] + ranks[1]["image_checksums"]
+    assert got == [float(x.double().sum()) for x in ref]

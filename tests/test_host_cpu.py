@@ -41,6 +41,32 @@ def test_c_abi_rejects_bad_shapes_before_touching_the_device():
         _lib.check(st)
 
 
+def test_c_abi_rejects_timing_and_layout2_configs():
+    """The product library exposes only tile configs that compute the GEMM on layout-1 weights:
+    the tuning build's timing-only variants (27/28 no unpack, 70-73 no MFMA / no restaging) and the
+    layout-2 v4 kernels (41-45) are rejected before any device work (no launch happens)."""
+    from samq import _lib, ops
+    from samq.quant_linear import QuantLinear
+    lib = _lib.load()
+    p = ctypes.c_void_p(4096)
+    for cfg in range(1, 100):
+        if cfg in ops.W4A16_CFGS:
+            continue
+        st = lib.samq_w4a16_gemm_cfg(p, 1280, p, p, p, None, p, 1280, 256, 1280, 1280, -1, 0, cfg, None)
+        assert st == _lib.SAMQ_ERR_INVALID, cfg
+    assert "unknown tile config" in lib.samq_last_error().decode() or "N not divisible" in lib.samq_last_error().decode()
+    for cfg in (27, 41, 71):
+        st = lib.samq_w4a16_gemm_cfg(p, 1280, p, p, p, None, p, 1280, 256, 1280, 1280, -1, 0, cfg, None)
+        assert st == _lib.SAMQ_ERR_INVALID
+    assert lib.samq_w4_repack_layout(p, p, 1280, 1280, 2, None) == _lib.SAMQ_ERR_INVALID
+    q = QuantLinear(4, -1, 256, 256, True)
+    for cfg in (71, 41, 27):
+        with pytest.raises(ValueError):
+            q.gemm_cfg = cfg
+    q.gemm_cfg = 22
+    assert q.gemm_cfg == 22
+
+
 @pytest.mark.parametrize("tag,g", [("gm1", -1), ("g128", 128)])
 def test_product_packer_bit_exact_vs_reference(golden_dir, tag, g):
     from samq.gptq import pack_linear, rtn

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: each GPU step under its own time limit; a crash / abort / timeout
 # (exit status other than 0 = pass or 1 = test failures) stops the session immediately.
-# usage: tools/gpu_session.sh <step> [<step> ...]   steps: kernels encoder bench smoke prof pmc
+# usage: tools/gpu_session.sh <step> [<step> ...]   steps: kernels encoder gpu bench smoke instep prof
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -30,6 +30,7 @@ for step in "$@"; do
     bench48) run bench_w4a8 600 python bench.py --mode w4a8 --steps 10 --warmup 3 ;;
     bench88) run bench_w8a8 600 python bench.py --mode w8a8 --steps 20 --warmup 5 ;;
     benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    instep)  run instep 500 bash tools/instep_profile.sh w4a16 ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
