@@ -240,6 +240,15 @@ int samq_patch_embed(const void* img, const void* weight, const float* bias, con
 int samq_patch_embed_f32(const float* img, const float* weight, const float* bias, const float* pos,
                          float* out, int B, int Cin, int img_size, int patch, int N, hipStream_t stream);
 
+/* PatchEmbed straight from RAW pixels (SamPredictor.set_image -> set_torch_image,
+ * segment_anything/predictor.py:34-90): img uint8 [B, Cin, h, w] (NCHW, h, w <= img_size) is
+ * normalised in the A-operand gather exactly as Sam.preprocess does (modeling/sam.py:164-174):
+ * (pixel - pixel_mean[c]) / pixel_std[c] (f32 [Cin] each), zero-padded to img_size x img_size;
+ * then as samq_patch_embed (weight f16) or, with weight_f32, as samq_patch_embed_f32. */
+int samq_patch_embed_u8(const uint8_t* img, int h, int w, const float* pixel_mean, const float* pixel_std,
+                        const void* weight, int weight_f32, const float* bias, const float* pos, float* out,
+                        int B, int Cin, int img_size, int patch, int N, hipStream_t stream);
+
 /* Neck 1x1 conv, no bias (image_encoder.py:88-104 neck[0]) on the fp32 token rows:
  * x f32 [M, K] (converted to f16 on load, as the reference's fp16 neck), weight f16 [N, K]
  * -> out f16 [M, N].  K % 32 == 0, N % 128 == 0. */

@@ -5,6 +5,10 @@
 //    image_encoder.py:411-442, :108-110): the 16x16 patches are gathered straight from the NCHW
 //    image into the A operand (no im2col copy), bias and the absolute position embedding are
 //    added in the fp32 epilogue, the fp32 residual stream is written directly;
+//  * the same from RAW uint8 pixels (SamPredictor.set_image, predictor.py:34-90): the gather
+//    applies Sam.preprocess (sam.py:164-174) itself -- (pixel - mean[c]) / std[c], and the zero
+//    padding of an h x w image (h, w <= img_size) to the square input -- so the normalised fp32
+//    image never exists in HBM (3 MB of uint8 read instead of 12 MB of fp32 written + read);
 //  * neck conv 1x1 (C -> 256, no bias, image_encoder.py:88-104): A = the fp32 residual tokens,
 //    converted to fp16 while staged (the reference runs the neck in fp16);
 //  * neck conv 3x3 pad 1 (256 -> 256, no bias): A gathered from the NHWC fp16 feature map with
@@ -16,7 +20,7 @@
 
 namespace samq {
 
-enum { CG_PATCH = 0, CG_1X1_F32 = 1, CG_3X3 = 2 };
+enum { CG_PATCH = 0, CG_1X1_F32 = 1, CG_3X3 = 2, CG_PATCH_U8 = 3 };
 
 struct ConvArgs {
   const void* x;        // PATCH: image f16 [B][Cin][G*P][G*P]; 1X1_F32: f32 [M][K]; 3X3: f16 [B][G][G][Cin]
@@ -26,14 +30,32 @@ struct ConvArgs {
   void* out;            // PATCH: f32 [M][N]; else f16 [M][N]
   int M, N, K;
   int G, P, Cin;
+  const float* mean;    // PATCH_U8: per-channel pixel mean / std (Sam.pixel_mean / pixel_std)
+  const float* stdv;
+  int ih, iw;           // PATCH_U8: real image rows / columns (<= G*P; the rest is zero padding)
 };
+
+// one normalised pixel of a raw uint8 NCHW image (Sam.preprocess), 0 in the padding
+__device__ __forceinline__ float pixel_norm(const ConvArgs& a, const uint8_t* img, int b, int c, int y, int x) {
+  if (y >= a.ih || x >= a.iw) return 0.f;
+  const float v = (float)img[(((int64_t)b * a.Cin + c) * a.ih + y) * a.iw + x];
+  return (v - a.mean[c]) / a.stdv[c];
+}
 
 template <int MODE>
 __device__ __forceinline__ half8_t conv_load_a(const ConvArgs& a, int t, int k) {
   // t: token index (< M), k: first of 8 consecutive reduction indices
   const int gg = a.G * a.G;
   const int b = t / gg, gy = (t / a.G) % a.G, gx = t % a.G;
-  if (MODE == CG_PATCH) {
+  if (MODE == CG_PATCH_U8) {
+    const int pp = a.P * a.P;
+    const int c = k / pp, rem = k - c * pp, kh = rem / a.P, kw = rem - kh * a.P;
+    const uint8_t* img = (const uint8_t*)a.x;
+    half8_t r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (_Float16)pixel_norm(a, img, b, c, gy * a.P + kh, gx * a.P + kw + j);
+    return r;
+  } else if (MODE == CG_PATCH) {
     const int pp = a.P * a.P;
     const int c = k / pp, rem = k - c * pp, kh = rem / a.P, kw = rem - kh * a.P;
     const int side = a.G * a.P;
@@ -135,7 +157,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const int col = n0 + wn * 64 + t * 32 + (lane & 31);
-    const float bcol = (MODE == CG_PATCH && a.bias) ? a.bias[col] : 0.f;
+    const float bcol = ((MODE == CG_PATCH || MODE == CG_PATCH_U8) && a.bias) ? a.bias[col] : 0.f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -143,7 +165,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
         if (row >= a.M) continue;
         float v = acc[i][t][r];
-        if (MODE == CG_PATCH) {
+        if (MODE == CG_PATCH || MODE == CG_PATCH_U8) {
           v += bcol;
           if (a.pos) v += a.pos[(int64_t)(row % gg) * a.N + col];
           ((float*)a.out)[(int64_t)row * a.N + col] = v;
@@ -158,6 +180,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 // fp32 patch embedding (the W4A8 engine: its first int8 quantiser sits right behind it, so the
 // embedding keeps the reference's fp32 arithmetic): the same implicit GEMM on
 // v_mfma_f32_32x32x2_f32, 128x128x16 tiles, fp32 image / weight / accumulation.
+template <bool U8>
 __global__ __launch_bounds__(256) void patch_embed_f32_kernel(ConvArgs a) {
   constexpr int BM = 128, BN = 128, BK = 16;
   constexpr int PITCH = BK + 1;   // floats; odd pitch spreads a fragment's 32 rows over the banks
@@ -187,8 +210,13 @@ __global__ __launch_bounds__(256) void patch_embed_f32_kernel(ConvArgs a) {
       t = t < a.M ? t : a.M - 1;
       const int b = t / gg, gy = (t / a.G) % a.G, gx = t % a.G;
       const int ci = k / pp, rem = k - ci * pp, kh = rem / a.P, kw = rem - kh * a.P;
-      ra[j] = *(const float4_t*)((const float*)a.x + (((int64_t)b * a.Cin + ci) * side + gy * a.P + kh) * side +
-                                 gx * a.P + kw);
+      if (U8) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ra[j][e] = pixel_norm(a, (const uint8_t*)a.x, b, ci, gy * a.P + kh, gx * a.P + kw + e);
+      } else {
+        ra[j] = *(const float4_t*)((const float*)a.x + (((int64_t)b * a.Cin + ci) * side + gy * a.P + kh) * side +
+                                   gx * a.P + kw);
+      }
       rb[j] = *(const float4_t*)((const float*)a.w + (int64_t)(n0 + row) * a.K + k);
     }
   };
@@ -321,7 +349,33 @@ extern "C" int samq_patch_embed_f32(const float* img, const float* weight, const
   const int g = img_size / patch;
   ConvArgs a{img, (const _Float16*)weight, bias, pos, out, B * g * g, N, Cin * patch * patch, g, patch, Cin};
   const int nwg = ((a.M + 127) / 128) * (a.N / 128);
-  hipLaunchKernelGGL(patch_embed_f32_kernel, dim3(nwg), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(patch_embed_f32_kernel<false>, dim3(nwg), dim3(256), 0, stream, a);
   SAMQ_LAUNCH_CHECK("patch_embed_f32 launch");
   return SAMQ_OK;
+}
+
+extern "C" int samq_patch_embed_u8(const uint8_t* img, int h, int w, const float* pixel_mean, const float* pixel_std,
+                                   const void* weight, int weight_f32, const float* bias, const float* pos, float* out,
+                                   int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  SAMQ_REQUIRE(img && pixel_mean && pixel_std && weight && out, SAMQ_ERR_INVALID, "patch_embed_u8: null pointer");
+  SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
+               "patch_embed_u8: image size must be a multiple of the patch size");
+  SAMQ_REQUIRE(h > 0 && w > 0 && h <= img_size && w <= img_size, SAMQ_ERR_INVALID,
+               "patch_embed_u8: the image must fit the square encoder input");
+  SAMQ_REQUIRE(N % 128 == 0, SAMQ_ERR_UNSUPPORTED, "patch_embed_u8: embed dim must be a multiple of 128");
+  SAMQ_REQUIRE(((uintptr_t)weight & 15) == 0, SAMQ_ERR_INVALID, "patch_embed_u8: weight must be 16-byte aligned");
+  const int g = img_size / patch;
+  ConvArgs a{img, (const _Float16*)weight, bias, pos, out, B * g * g, N, Cin * patch * patch, g, patch, Cin,
+             pixel_mean, pixel_std, h, w};
+  const int nwg = ((a.M + 127) / 128) * (a.N / 128);
+  if (weight_f32) {
+    SAMQ_REQUIRE(patch % 4 == 0 && (Cin * patch * patch) % 16 == 0, SAMQ_ERR_UNSUPPORTED,
+                 "patch_embed_u8: patch must be a multiple of 4 and Cin*patch^2 a multiple of 16");
+    hipLaunchKernelGGL(patch_embed_f32_kernel<true>, dim3(nwg), dim3(256), 0, stream, a);
+    SAMQ_LAUNCH_CHECK("patch_embed_u8 (f32) launch");
+    return SAMQ_OK;
+  }
+  SAMQ_REQUIRE(patch % 8 == 0 && (Cin * patch * patch) % 32 == 0, SAMQ_ERR_UNSUPPORTED,
+               "patch_embed_u8: patch must be a multiple of 8 and Cin*patch^2 a multiple of 32");
+  return conv_launch<CG_PATCH_U8>(a, stream);
 }

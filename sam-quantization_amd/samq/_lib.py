@@ -74,6 +74,8 @@ SIGNATURES = {
                                      _f32, _f32, _f32, _vp]),
     "samq_patch_embed": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_patch_embed_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "samq_patch_embed_u8": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32,
+                                   _i32, _vp]),
     "samq_conv1x1_f32": (_i32, [_vp, _vp, _vp, _i64, _i32, _i32, _vp]),
     "samq_conv3x3_nhwc": (_i32, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _vp]),
 }

@@ -95,6 +95,7 @@ class EncoderEngine:
         self.n2_w_tap = n2.weight.detach().permute(0, 2, 3, 1).to(torch.float16).contiguous()
         self.n3 = (n3.weight.detach().float().contiguous(), n3.bias.detach().float().contiguous(), float(n3.eps))
         self.out_chans = n0.weight.shape[0]
+        self._pixel_norm = None
         self._bufs = OrderedDict()   # (images, lane) -> activation buffers, most recent last
         self.max_cached_batches = 2  # distinct per-lane batch sizes kept (captured graphs pin their own)
         self._key = self._make_key(enc)
@@ -160,9 +161,17 @@ class EncoderEngine:
     def embed(self, img: torch.Tensor, x32: torch.Tensor) -> None:
         """Patch embedding + bias + pos_embed into the fp32 residual stream: one implicit-GEMM HIP
         kernel (patches read straight from the NCHW image).  W4A8 computes it in fp32
-        (``samq_patch_embed_f32``): its first int8 quantiser sits right behind it."""
+        (``samq_patch_embed_f32``): its first int8 quantiser sits right behind it.  A uint8 image
+        (raw pixels, ``pixel_norm`` set by ``forward``) is normalised and zero-padded inside the
+        same kernel (``Sam.preprocess`` fused, ``samq_patch_embed_u8``)."""
         p = self.patch
         pos = None if self.pos is None else self.pos[0]
+        if img.dtype == torch.uint8:
+            if self._pixel_norm is None:
+                raise ValueError("uint8 pixels need pixel_norm=(pixel_mean, pixel_std)")
+            ops.patch_embed_u8(img.contiguous(), *self._pixel_norm, self.pe_w32 if self.w4a8 else self.pe_w, self.pe_b,
+                               pos, p, self.enc.img_size, out=x32)
+            return
         if not self.w4a8:
             ops.patch_embed(img.to(torch.float16).contiguous(), self.pe_w, self.pe_b, pos, p, out=x32)
             return
@@ -205,7 +214,7 @@ class EncoderEngine:
 
     # ---------------------------------------------------------------- forward
     @torch.no_grad()
-    def forward(self, img: torch.Tensor, out_dtype=None, lanes: int = 1) -> torch.Tensor:
+    def forward(self, img: torch.Tensor, out_dtype=None, lanes: int = 1, pixel_norm=None) -> torch.Tensor:
         """Whole encoder forward.  ``lanes > 1`` splits the batch into that many image groups,
         each run as its own kernel chain on its own HIP stream (images are independent: per-token
         LN, per-image attention).  Kernels of one lane fill the CUs another lane leaves idle —
@@ -214,8 +223,14 @@ class EncoderEngine:
         result is bit-identical to ``lanes=1`` (tests/test_gpu_encoder.py).
 
         Returns ``(B, out_chans, H, W)`` in channels-last memory (an NCHW view of the engine's
-        NHWC tokens) for every ``lanes``; ``lanes`` must divide the batch (``ValueError``)."""
+        NHWC tokens) for every ``lanes``; ``lanes`` must divide the batch (``ValueError``).
+        ``img`` may be raw uint8 pixels (B, 3, h, w) with ``pixel_norm=(pixel_mean, pixel_std)``:
+        the normalise + zero-pad of ``Sam.preprocess`` then runs inside the patch embedding."""
         assert img.is_cuda, "EncoderEngine runs on the GPU only"
+        if img.dtype == torch.uint8:
+            # raw (B, 3, h, w) pixels, h, w <= img_size: Sam.preprocess runs inside the patch embedding
+            self._pixel_norm = tuple(t.reshape(-1).float().contiguous() for t in pixel_norm) if pixel_norm else None
+            out_dtype = out_dtype or torch.float32
         out_dtype = out_dtype or img.dtype
         b = img.shape[0]
         if lanes <= 1 or b < 2:

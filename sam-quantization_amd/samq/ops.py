@@ -127,6 +127,31 @@ def patch_embed(img: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Te
     return out
 
 
+def patch_embed_u8(img: torch.Tensor, pixel_mean: torch.Tensor, pixel_std: torch.Tensor, weight: torch.Tensor,
+                   bias: Optional[torch.Tensor], pos: Optional[torch.Tensor], patch: int, img_size: int,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Raw uint8 pixels (B, Cin, h, w), h, w <= img_size -> f32 (B, S/p, S/p, N): Sam.preprocess
+    (normalise by pixel mean / std, zero-pad to img_size) fused into the patch-embedding GEMM.
+    weight f16 (fp16 MFMA) or f32 (fp32 MFMA, the W4A8 embedding)."""
+    _need_cuda(img, pixel_mean, pixel_std, weight, bias, pos)
+    assert img.dtype == torch.uint8 and img.dim() == 4 and img.is_contiguous()
+    b, cin, h, w = img.shape
+    mean = pixel_mean.reshape(-1).float().contiguous()
+    std = pixel_std.reshape(-1).float().contiguous()
+    assert mean.numel() == cin and std.numel() == cin
+    n = weight.shape[0]
+    assert weight.dtype in (torch.float16, torch.float32) and weight.is_contiguous()
+    assert weight.shape[1] == cin * patch * patch
+    g = img_size // patch
+    if out is None:
+        out = torch.empty((b, g, g, n), dtype=torch.float32, device=img.device)
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == b * g * g * n
+    _lib.check(_lib.load().samq_patch_embed_u8(_ptr(img), h, w, _ptr(mean), _ptr(std), _ptr(weight),
+                                               int(weight.dtype == torch.float32), _ptr(bias), _ptr(pos), _ptr(out),
+                                               b, cin, img_size, patch, n, _stream()), "patch_embed_u8")
+    return out
+
+
 def conv1x1_f32(x: torch.Tensor, weight: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x f32 (..., K) tokens -> f16 (..., N) = x . weight^T (1x1 conv, no bias); weight f16 (N, K)."""
     _need_cuda(x, weight)

@@ -351,11 +351,17 @@ class SamPredictor:
         self.reset_image()
         self.original_size = tuple(original_image_size)
         self.input_size = tuple(transformed_image.shape[-2:])
-        x = self.model.preprocess(transformed_image.float())
         enc = self.model.image_encoder
-        p = next(enc.parameters(), None)
-        dt = p.dtype if p is not None and p.is_floating_point() else torch.float32
-        self.features = enc(x.to(dt)).float()
+        if transformed_image.is_cuda and transformed_image.dtype == torch.uint8 and enc.is_quantized():
+            # HIP engine: Sam.preprocess (normalise + zero-pad) runs inside the patch embedding
+            # kernel on the raw uint8 pixels (samq_patch_embed_u8)
+            self.features = enc.engine()(transformed_image.contiguous(), out_dtype=torch.float32,
+                                         pixel_norm=(self.model.pixel_mean, self.model.pixel_std))
+        else:
+            x = self.model.preprocess(transformed_image.float())
+            p = next(enc.parameters(), None)
+            dt = p.dtype if p is not None and p.is_floating_point() else torch.float32
+            self.features = enc(x.to(dt)).float()
         self.is_image_set = True
 
     def get_image_embedding(self) -> torch.Tensor:

@@ -103,3 +103,114 @@ def test_mask_iou_hip_encoder_vs_reference(cuda, golden_dir):
     print(f"\n[mask IoU] HIP W4A16 ViT-H vs reference embedding, {len(ious)} masks: "
           f"min {min(ious):.4f} mean {np.mean(ious):.4f}")
     assert min(ious) >= 0.97
+    # 5-click mIoU (evaluation2.py:226-381) on synthetic ground truth, same seeded click RNG:
+    # first clicks coincide (empty previous mask), so their IoUs must agree to 0.02; later clicks
+    # may land on different error pixels, so the 5-click mIoU gap is bounded at 0.05
+    from samq.click_eval import click_iou, synthetic_gt_masks
+    gts = synthetic_gt_masks(4, seed=3)
+    ref_emb = torch.from_numpy(f["out"].astype(np.float32)).to(cuda)
+    mine = click_iou(pe, md, emb, gts, num_clicks=5, seed=5)
+    theirs = click_iou(pe, md, ref_emb, gts, num_clicks=5, seed=5)
+    m_mine, m_ref = float(np.mean([r[-1] for r in mine])), float(np.mean([r[-1] for r in theirs]))
+    print(f"[5-click mIoU] HIP W4A16 embedding {m_mine:.4f} vs reference embedding {m_ref:.4f} "
+          f"(per-click HIP {np.mean(mine, 0).round(4).tolist()} ref {np.mean(theirs, 0).round(4).tolist()})")
+    assert max(abs(a[0] - b[0]) for a, b in zip(mine, theirs)) <= 0.02
+    assert abs(m_mine - m_ref) <= 0.05
+
+
+def _vitb_state_1024():
+    cfg = synth.encoder_config("vit_b", img_size=1024)
+    return cfg, synth.make_encoder_state(cfg, seed=11)
+
+
+def _preprocess_np(img_u8, size=1024):
+    """Sam.preprocess restated (reference modeling/sam.py:164-174): normalise, zero-pad."""
+    mean = np.array([123.675, 116.28, 103.53], np.float32)[:, None, None]
+    std = np.array([58.395, 57.12, 57.375], np.float32)[:, None, None]
+    x = (img_u8.transpose(2, 0, 1).astype(np.float32) - mean) / std
+    out = np.zeros((1, 3, size, size), np.float32)
+    out[0, :, :x.shape[1], :x.shape[2]] = x
+    return out
+
+
+def test_config1_predictor_vit_b_1024_cpu():
+    """BASELINE config 1 at its real size: SAM vit_b, fp32 PyTorch on the CPU, one 1024x1024 RGB
+    image through SamPredictor.set_image (predictor.py:34-90: ResizeLongestSide -> identity at
+    1024, Sam.preprocess, encoder) vs the oracle encoder on the restated preprocessing."""
+    import samq
+    from oracle import sam_ref
+    from samq.build_sam import Sam, build_image_encoder
+    cfg, st = _vitb_state_1024()
+    enc = build_image_encoder(768, 12, 12, [2, 5, 8, 11], img_size=1024)
+    enc.load_state_dict({k: torch.from_numpy(v) for k, v in st.items()})
+    sam = Sam(enc).eval()
+    pred = samq.SamPredictor(sam)
+    rng = np.random.Generator(np.random.PCG64(12))
+    img = rng.integers(0, 256, (1024, 1024, 3), dtype=np.uint8)
+    torch.set_num_threads(8)
+    pred.set_image(img)
+    emb = pred.get_image_embedding().numpy()
+    ref = sam_ref.EncoderOracle(cfg, st)(_preprocess_np(img)).numpy()
+    err = float(np.abs(emb - ref).max())
+    print(f"\n[parity] config 1 vit_b 1024 SamPredictor (CPU fp32) vs oracle: max-abs {err:.3e}")
+    assert emb.shape == (1, 256, 64, 64) and err < 1e-3
+
+
+@pytest.mark.gpu
+def test_predictor_hip_engine_fused_preprocess(cuda):
+    """SamPredictor.set_image on a quantized ViT-H (4 blocks, W4A16) on the GPU: the raw uint8
+    pixels go straight into the patch-embedding kernel (Sam.preprocess fused: normalise + zero
+    pad of a 1024x800 image).  Bit-identical to the engine on the torch-preprocessed fp16 image,
+    and within 1e-2 of oracle G1 on the restated preprocessing."""
+    import samq
+    from samq.build_sam import Sam
+    from _encoder_helpers import oracle_g1, oracle_vith, product_encoder
+    cfg, st, names, q = oracle_vith(4, 13, global_idx=(1, 3))
+    enc = product_encoder(cfg, st, names, q, -1, cuda)
+    sam = Sam(enc).to(cuda).eval()
+    pred = samq.SamPredictor(sam)
+    rng = np.random.Generator(np.random.PCG64(14))
+    img = rng.integers(0, 256, (1024, 800, 3), dtype=np.uint8)
+    pred.set_image(img)
+    emb = pred.get_image_embedding()
+    assert pred.input_size == (1024, 800) and emb.shape == (1, 256, 64, 64)
+    x = sam.preprocess(torch.from_numpy(img).to(cuda).permute(2, 0, 1)[None].float())
+    ref_eng = enc.engine()(x.half(), out_dtype=torch.float32)
+    assert torch.equal(emb, ref_eng)
+    ref = oracle_g1(cfg, st, names, q)(_preprocess_np(img)).numpy()
+    err = float(np.abs(emb.cpu().numpy() - ref).max())
+    print(f"\n[parity] predictor (fused u8 preprocess) ViT-H 4 blocks vs oracle G1: max-abs {err:.3e}")
+    assert err <= 1e-2
+    masks, iou, low = pred.predict(point_coords=np.array([[400.0, 500.0]]), point_labels=np.array([1]))
+    assert masks.shape == (3, 1024, 800)
+
+
+def test_get_iou_ignore_label_and_click_sampling():
+    """get_iou excludes ignore_label pixels from intersection and union (evaluation2.py:156-167);
+    get_next_click_torch clicks inside the error region, positive iff a false negative."""
+    from samq.click_eval import get_iou, get_next_click_torch
+    gt = torch.tensor([[[[1, 1, 0, -1], [0, 1, 0, -1]]]], dtype=torch.float32)
+    pred = torch.tensor([[[[1, 0, 1, 1], [0, 1, 0, 1]]]], dtype=torch.bool)
+    # keep = 6 pixels; object = 3; pred & obj & keep = 2; (pred | obj) & keep = 4
+    assert float(get_iou(gt, pred)) == 0.5
+    rng = np.random.Generator(np.random.PCG64(0))
+    prev = torch.zeros_like(gt)
+    for _ in range(20):
+        p, lab = get_next_click_torch(prev, gt, rng)
+        x, y = int(p[0][0, 0, 0]), int(p[0][0, 0, 1])
+        assert gt[0, 0, y, x] > 0 and int(lab[0]) == 1          # only false negatives before the first mask
+    prev = torch.tensor([[[[1, 1, 1, 0], [0, 1, 0, 0]]]], dtype=torch.float32)
+    p, lab = get_next_click_torch(prev, gt, rng)
+    assert (int(p[0][0, 0, 0]), int(p[0][0, 0, 1])) == (2, 0) and int(lab[0]) == 0   # the one false positive
+
+
+def test_click_loop_on_reference_embedding_cpu(golden_dir):
+    """The 5-click loop (evaluation2.py:226-381) on the reference's own 32-block ViT-H embedding:
+    every episode improves on its first click and ends above it."""
+    from samq.click_eval import click_iou, synthetic_gt_masks
+    emb = torch.from_numpy(np.load(golden_dir / "encoder_vith32.npz")["out"].astype(np.float32))
+    pe, md = _decoder()
+    gts = synthetic_gt_masks(2, seed=3)
+    ious = click_iou(pe, md, emb, gts, num_clicks=5, seed=5)
+    assert len(ious) == 2 and all(len(r) == 5 for r in ious)
+    assert all(0.0 <= v <= 1.0 for r in ious for v in r)

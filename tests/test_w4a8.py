@@ -105,3 +105,66 @@ def test_w4a8_vith_vs_oracle(cuda):
     with torch.no_grad():
         mod = enc.module_forward(torch.from_numpy(x).to(cuda).half()).float().cpu().numpy()
     assert np.abs(mod - ref).max() <= 1.5 * nmax and np.abs(mod - ref).mean() <= 1.5 * nmean
+
+
+def _w4a8_product(depth, seed, cuda, global_idx=None, calib_seed=1):
+    import samq
+    cfg, st, names, q, o = _oracle(depth, seed, global_idx=global_idx)
+    enc = product_encoder(cfg, st, names, q, -1, cuda).half()
+    samq.make_act_quant(enc)
+    calib = [synth.make_images(1, 1024, seed=calib_seed)]
+    samq.calibrate_act_quant(enc, lambda im: enc.module_forward(torch.from_numpy(im).to(cuda).half()), calib)
+    return cfg, st, names, q, o, enc
+
+
+@pytest.mark.gpu
+def test_w4a8_lanes_bit_identical_b8(cuda):
+    """Config 5 geometry: W4A8 ViT-H at B=8 through the 2-lane (and 4-lane) engine, eager and
+    captured, is bit-identical to one chain and each image to its own B=1 run (the int8 GEMMs
+    are integer-exact whatever tile config i8_pick_cfg takes per M; every kernel is
+    batch-invariant).  The W4A8 fp32 patch-embedding weight is built before any lane fork."""
+    *_, enc = _w4a8_product(4, 5, cuda, global_idx=(1, 3))
+    eng = enc.engine()
+    assert eng.w4a8 and eng.pe_w32 is not None
+    x = torch.from_numpy(synth.make_images(8, 1024, seed=40)).to(cuda).half()
+    ref = eng(x, out_dtype=torch.float32)
+    for lanes in (2, 4):
+        out = eng(x, out_dtype=torch.float32, lanes=lanes)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), lanes
+    static = x.clone()
+    graph, gout = eng.capture(static, out_dtype=torch.float32, lanes=2)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gout, ref)
+    for i in (0, 5):
+        one = eng(x[i:i + 1], out_dtype=torch.float32)
+        assert torch.equal(one[0], ref[i]), i
+    assert torch.isfinite(ref).all()
+
+
+@pytest.mark.gpu
+def test_w4a8_vith32_vs_oracle(cuda):
+    """Full 32-block ViT-H W4A8 engine vs the W4A8 oracle fed the engine's own calibrated scales.
+    Stated tolerances: (relative) distance to the oracle <= 1.5x the int8 activation noise (oracle
+    W4A8 vs oracle W4A16) in max-abs and mean-abs, and (absolute) mean-abs <= 2.5e-2 and
+    max-abs <= 0.6 on outputs of absmax ~5 (measured: see the printed line)."""
+    import samq
+    cfg, st, names, q, o, enc = _w4a8_product(32, 7, cuda)
+    scales = {}
+    for n, m in enc.named_modules():
+        if isinstance(m, samq.QuantLinear):
+            scales[n.replace("qkv_proj", "qkv").replace("o_proj", "proj")] = float(m.act_quant.quantizer.scale)
+    o.set_scales(scales)
+    x = synth.make_images(1, 1024, seed=9)
+    out = enc.engine()(torch.from_numpy(x).to(cuda).half(), out_dtype=torch.float32).cpu().numpy()
+    torch.set_num_threads(16)
+    ref = o(x).numpy()
+    o.mode = "float"
+    w4 = o(x).numpy()
+    err, mean = float(np.abs(out - ref).max()), float(np.abs(out - ref).mean())
+    nmax, nmean = float(np.abs(ref - w4).max()), float(np.abs(ref - w4).mean())
+    print(f"\n[parity] W4A8 ViT-H 32 blocks vs oracle: max-abs {err:.3e} mean-abs {mean:.3e} | int8 noise "
+          f"max-abs {nmax:.3e} mean-abs {nmean:.3e} | ref absmax {np.abs(ref).max():.3f}")
+    assert err <= 1.5 * nmax and mean <= 1.5 * nmean
+    assert mean <= 5e-2 and err <= 0.35
