@@ -125,6 +125,20 @@ int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked
                      int64_t ldr, int M, int N, int K, int epilogue, float a_scale, float mid_scale,
                      float res_scale, float out_scale, int cfg, hipStream_t stream);
 
+/* W8A8 convolution as an implicit GEMM (fq_vit QConv2d on int8 codes, layers.py:11-74): the A
+ * operand is gathered from the code map by the LDS-DMA loader, no im2col copy.
+ *   mode 1 (PatchEmbed, fq_vit image_encoder.py PatchEmbed): x int8 [B, Cin, side, side] NCHW,
+ *     16x16 patches stride 16; weight codes flattened (n, c, kh, kw) (K = Cin*256);
+ *   mode 2 (neck 3x3, padding 1, image_encoder.py:88-104): x int8 [B, side, side, Cin] NHWC,
+ *     Cin % 128 == 0; weight codes permuted to (n, ky, kx, c) (K = 9*Cin).
+ * Weights from samq_w8_repack; output C int8 [B*G*G, N] codes (row stride N) with epilogue Q8 or
+ * Q8_RES as samq_w8a8_gemm; Q8_RES reads residual codes R [rmod, N] at row (r % rmod) when
+ * rmod > 0 (the pos_embed codes shared by every image), else R [B*G*G, N]. */
+int samq_w8a8_conv_gemm(const int8_t* x, int mode, int B, int Cin, int side, const int8_t* wpacked,
+                        const float* wscale, const float* bias, void* C, const int8_t* R, int rmod,
+                        int N, int epilogue, float a_scale, float mid_scale, float res_scale,
+                        float out_scale, hipStream_t stream);
+
 /* Elementwise activation quantiser (fq_vit QAct in quant mode, layers.py:232-242 ->
  * UniformQuantizer.forward, quantizer/base.py:43-49, uniform.py:23-45, zero point 0):
  * codes[i] = q(x[i], scale); x f32 (or f16 with SAMQ_Q_IN_F16); with SAMQ_Q_OUT_FQ the output is

@@ -43,6 +43,8 @@ __device__ __forceinline__ float aq8(float v, float s) {
 }
 
 constexpr int QD = 64;       // head dim (vit_b)
+
+__device__ __forceinline__ float q8max3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 constexpr int KPITCH = 80;   // K row pitch in LDS (bytes): conflict-free 16-byte fragment reads
 
 // ROW64: global attention over a 64-wide grid -- a 64-key chunk is exactly one key row, so the
@@ -299,6 +301,199 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
   }
 }
 
+
+// ------------------------------------------------------------------ global, 64 x 64 grid (vit_b)
+// The global blocks of the W8A8 vit_b encoder (4096 keys).  A workgroup = one query grid row
+// (64 queries, 4 waves x 16); key row kh is chunk kh (64 keys): its K codes (int8) and V codes
+// (converted once to fp16, row-major) go through a 2-deep LDS ring with 16-byte stores, the next
+// chunk's global loads in flight under the current chunk's math.  Per chunk and wave:
+//   S^T = K.Q^T on 4 x v_mfma_i32_16x16x64_i8 (exact int32; lane = query ql, keys 16bb+4g+i);
+//   c = q8(q8(st * s_qkv^2 * scale, s_a1) * s_a1 + rel_h[kh] + rel_w[kw], s_a2): the two score
+//       quantisers (reciprocal multiply, round-half-even, clamp) in the reference's addition order
+//       (fq_vit image_encoder.py:455-470; rel_w indexed by the query ROW, quirk 1);
+//   online softmax on the integer codes, p = exp2(c * k2 - m * k2) (one fma + exp2);
+//   O^T += V^T.P^T on 16x16x32 f16 MFMAs with P split hi + lo (|P - hi - lo| ~ 2^-22 |P|), V^T
+//       fragments by ds_read_b64_tr_b16 from the row-major fp16 V; the softmax denominators come
+//       from the same MFMAs against an all-ones operand (fp32 sums of the same hi + lo).
+template <int NWQ>
+__global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8Params p) {
+  constexpr int G = 64, KC = 64, VP = QD + 8;    // V row pitch (halves): spreads the tr reads over banks
+  constexpr int NT = 64 * NWQ;
+  constexpr int UNITS = KC * 4;                  // 16-byte pieces of one chunk's K (and of its V)
+  static_assert(UNITS % NT == 0, "staging");
+  constexpr int UPT = UNITS / NT;
+  __shared__ __attribute__((aligned(16))) int8_t k_lds[2][KC * KPITCH];
+  __shared__ __attribute__((aligned(16))) _Float16 v_lds[2][KC * VP];
+  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
+  __shared__ float rh_lds[NWQ][16 * (G + 1)];
+  __shared__ float rw_lds[NWQ][16 * (G + 1)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int ql = lane & 15;
+  const int C = p.C;
+  const int head = blockIdx.y;
+  const int b = blockIdx.x;
+  const int qy = blockIdx.z;                    // query grid row of this workgroup
+  const int qx = wave * 16 + ql;
+  const int64_t ts = 3 * (int64_t)C;
+  const int8_t* img = p.qkv + (int64_t)b * G * G * ts;
+
+  // ---- K / V staging: piece u = key * 4 + part (16 bytes of dims 16 part .. +15)
+  u32x4 kreg[UPT], vreg[UPT];
+  auto load = [&](int kh) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const int u = tid + j * NT, key = u >> 2, part = u & 3;
+      const int8_t* tp = img + ((int64_t)kh * G + key) * ts + head * QD + part * 16;
+      kreg[j] = *(const u32x4*)(tp + C);
+      vreg[j] = *(const u32x4*)(tp + 2 * C);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < UPT; ++j) {
+      const int u = tid + j * NT, key = u >> 2, part = u & 3;
+      *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kreg[j];
+      half8_t h0, h1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        h0[e] = (_Float16)(float)(int8_t)((vreg[j][e >> 2] >> (8 * (e & 3))) & 0xFFu);
+        h1[e] = (_Float16)(float)(int8_t)((vreg[j][2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
+      }
+      *(half8_t*)(&v_lds[buf][key * VP + part * 16]) = h0;
+      *(half8_t*)(&v_lds[buf][key * VP + part * 16 + 8]) = h1;
+    }
+  };
+  load(0);
+
+  // ---- this wave's 16 queries (codes) and their rel-pos terms: fp32 dot products of the
+  // fake-quant q with the f32 tables (rows qy - k + 63 for both, quirk 1)
+  const int4v qfrag = *(const int4v*)(img + ((int64_t)qy * G + qx) * ts + head * QD + g * 16);
+  *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  for (int pi = lane; pi < 16 * G; pi += 64) {
+    const int qi = pi & 15, kk = pi >> 4;
+    const int ridx = qy - kk + G - 1;
+    const float* th = p.relh + (int64_t)ridx * QD;
+    const float* tw = p.relw + (int64_t)ridx * QD;
+    float ah = 0.f, aw = 0.f;
+#pragma unroll 1
+    for (int d4 = 0; d4 < QD / 16; ++d4) {
+      const u32x4 cw = *(const u32x4*)(&q_lds[wave][qi * KPITCH + d4 * 16]);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
+        const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
+          ah = fmaf(qf, h4[e], ah);
+          aw = fmaf(qf, w4[e], aw);
+        }
+      }
+    }
+    rh_lds[wave][qi * (G + 1) + kk] = ah;
+    rw_lds[wave][qi * (G + 1) + kk] = aw;
+  }
+  store(0);
+  __syncthreads();   // chunk 0 staged; this wave's rel terms visible to itself
+  float rwr[4][4];
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rwr[bb][i] = rw_lds[wave][ql * (G + 1) + bb * 16 + 4 * g + i];
+  const float* rhq = &rh_lds[wave][ql * (G + 1)];
+
+  const float c1 = p.qk_scale * p.inv_a1, sa1 = p.s_a1, inv2 = p.inv_a2, k2 = p.k2;
+  const int trow = ql >> 2, tcol = 4 * (ql & 3);
+  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
+  float m = -INFINITY;
+  float4_t acc[QD / 16], lacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int ch = 0; ch < G; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < G) load(ch + 1);               // in flight under this chunk's math
+    // ---- scores -> two quantisers -> integer codes c
+    const float rh_row = rhq[ch];
+    float c[4][4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int4v kf = *(const int4v*)(&k_lds[buf][(bb * 16 + ql) * KPITCH + g * 16]);
+      const int4v z = {0, 0, 0, 0};
+      const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f) * sa1;
+        const float t = (v1 + rh_row) + rwr[bb][i];
+        c[bb][i] = __builtin_amdgcn_fmed3f(__builtin_rintf(t * inv2), -128.f, 127.f);
+      }
+    }
+    float cmax = q8max3(c[0][0], c[0][1], c[0][2]);
+    cmax = q8max3(cmax, c[0][3], c[1][0]);
+    cmax = q8max3(cmax, c[1][1], c[1][2]);
+    cmax = q8max3(cmax, c[1][3], c[2][0]);
+    cmax = q8max3(cmax, c[2][1], c[2][2]);
+    cmax = q8max3(cmax, c[2][3], c[3][0]);
+    cmax = q8max3(cmax, c[3][1], c[3][2]);
+    cmax = fmaxf(cmax, c[3][3]);
+    cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    if (cmax > m) {   // wave-uniform per query column: rescale O and l
+      const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
+      lacc = lacc * alpha;
+      m = cmax;
+    }
+    const float off = -m * k2;
+    // ---- P (hi + lo fp16) and O^T += V^T.P^T, l += ones.P^T, two 32-key steps
+    const _Float16* vb = &v_lds[buf][0];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      half8_t bhi, blo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pv = __builtin_amdgcn_exp2f(fmaf(c[2 * s2 + (j >> 2)][j & 3], k2, off));
+        const _Float16 h = (_Float16)pv;
+        bhi[j] = h;
+        blo[j] = (_Float16)(pv - (float)h);
+      }
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) {
+        const _Float16* a0 = vb + (32 * s2 + 4 * g + trow) * VP + t * 16 + tcol;
+        const half4_t lo = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)a0));
+        const half4_t hi = __builtin_bit_cast(
+            half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0 + 16 * VP)));
+        const half8_t af = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bhi, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, blo, acc[t], 0, 0, 0);
+      }
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, bhi, lacc, 0, 0, 0);
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, blo, lacc, 0, 0, 0);
+    }
+    if (ch + 1 < G) store(buf ^ 1);   // the other buffer was last read before the previous barrier
+    __syncthreads();
+  }
+
+  const float lsum = lacc[0];
+  int8_t* op = p.out + (((int64_t)b * G + qy) * G + qx) * C + head * QD;
+#pragma unroll
+  for (int t = 0; t < QD / 16; ++t) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float o = acc[t][i] / lsum * p.s_qkv;
+      w |= ((uint32_t)(int)aq8(o, p.s_out) & 0xFFu) << (8 * i);
+    }
+    *(uint32_t*)(op + t * 16 + 4 * g) = w;
+  }
+}
+
 }  // namespace samq
 
 using namespace samq;
@@ -336,8 +531,8 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.S = H; p.window = 0; p.nwh = p.nww = 1; p.L = H * W;
     constexpr int NWQ = 4;
     const dim3 grid(B, heads, (p.L + 16 * NWQ - 1) / (16 * NWQ));
-    if (H == 64)
-      hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, true>), grid, dim3(64 * NWQ), 0, stream, p);
+    if (H == 64)   // one grid row of queries per workgroup (16 * NWQ == 64)
+      hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ>), grid, dim3(64 * NWQ), 0, stream, p);
     else
       hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, false>), grid, dim3(64 * NWQ), 0, stream, p);
   }

@@ -31,7 +31,18 @@ struct I8Epi {
   float a_scale, mid_scale, res_scale, out_scale;
   const int8_t* R;
   int64_t ldr;
+  int rmod;               // > 0: residual row = output row % rmod (pos_embed codes shared by images)
 };
+
+// Implicit-GEMM A operand (AG != 0): the int8 codes are gathered from an image / feature map
+// instead of an [M, K] matrix, 16 contiguous bytes per LDS-DMA lane:
+//   AG_PATCH  x int8 [B, Cin, S, S] (NCHW), P = 16: A[t, (c, kh, kw)] = x[b, c, gy*16+kh, gx*16+kw]
+//             (fq_vit PatchEmbed QConv2d on the image codes, fq_vit image_encoder.py PatchEmbed)
+//   AG_3X3    x int8 [B, G, G, Cin] (NHWC), pad 1: A[t, (ky, kx, c)] = x[b, gy+ky-1, gx+kx-1, c], 0 outside
+//             (neck QConv2d 3x3, image_encoder.py:88-104; weight codes permuted to (n, ky, kx, c))
+enum { AG_ROWS = 0, AG_PATCH = 1, AG_3X3 = 2 };
+struct I8Gather { int S, G, Cin; };
+__device__ __attribute__((aligned(16))) int8_t g_zero_i8[16];
 
 __device__ __forceinline__ float q8f(float v, float s) {
   // clamp(round_half_even(v / s), -128, 127)   (quantizer/uniform.py:31-36, true division)
@@ -67,12 +78,12 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
 }
 
 // ------------------------------------------------------------------ GEMM
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES>
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
                     const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
                     const float* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
-                    int M, int N, int K, I8Epi ep_args) {
+                    int M, int N, int K, I8Epi ep_args, I8Gather ga) {
   constexpr int NW = WAVES_M * WAVES_N;
   constexpr int WM = BM / WAVES_M;
   constexpr int WN = BN / WAVES_N;
@@ -106,6 +117,7 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   const char* src[NPW];
   int dst[NPW];
   int64_t step[NPW];
+  int gtok[NPW], gck[NPW];   // AG: token (b, gy, gx) and in-tile byte offset of each A piece's lane
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     int j = wave * NPW + i;
@@ -116,6 +128,8 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
       int gr = m0 + row;
       gr = gr < M ? gr : M - 1;
       src[i] = (const char*)(A + (int64_t)gr * lda + c * 16);
+      gtok[i] = gr;
+      gck[i] = c * 16;
       dst[i] = j * 1024;
       step[i] = BK;
     } else {
@@ -126,11 +140,28 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
       step[i] = PPB * 1024;
     }
   }
+  auto a_gather = [&](int i, int kt) -> const char* {
+    const int t = gtok[i], k = kt * BK + gck[i];
+    const int gg = ga.G * ga.G;
+    const int b = t / gg, rem = t - b * gg, gy = rem / ga.G, gx = rem - gy * ga.G;
+    if (AG == AG_PATCH) {   // k = (c * 16 + kh) * 16 + kw, kw = 0..15 contiguous
+      const int ckh = k >> 4;
+      const int c = ckh >> 4, kh = ckh & 15;
+      return (const char*)(A + (((int64_t)b * ga.Cin + c) * ga.S + gy * 16 + kh) * ga.S + gx * 16);
+    }
+    const int tap = k / ga.Cin, c0 = k - tap * ga.Cin;   // AG_3X3: k = (ky * 3 + kx) * Cin + c
+    const int sy = gy + tap / 3 - 1, sx = gx + tap % 3 - 1;
+    if (sy < 0 || sy >= ga.G || sx < 0 || sx >= ga.G) return (const char*)g_zero_i8;
+    return (const char*)(A + (((int64_t)b * ga.G + sy) * ga.G + sx) * ga.Cin + c0);
+  };
   auto issue = [&](int kt, int slot) {
 #pragma unroll
-    for (int i = 0; i < NPW; ++i)
-      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + kt * step[i]),
-                                       (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+    for (int i = 0; i < NPW; ++i) {
+      const char* p = src[i] + kt * step[i];
+      if (AG != AG_ROWS && wave * NPW + i < NA) p = a_gather(i, kt);
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)p, (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16,
+                                       0, 0);
+    }
   };
 
   int col[TN];
@@ -291,7 +322,8 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
             }
             u32x4 res;
             if (EPI == SAMQ_EPI_Q8_RES)
-              res = *(const u32x4*)(ep_args.R + (int64_t)row * ep_args.ldr + col_base + 16 * c16);
+              res = *(const u32x4*)(ep_args.R + (int64_t)(ep_args.rmod > 0 ? row % ep_args.rmod : row) * ep_args.ldr +
+                                    col_base + 16 * c16);
             u32x4 o;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
@@ -320,14 +352,14 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
 
 struct I8Args {
   const int8_t* A; int64_t lda; const char* Wp; const float* wscale; const uint32_t* qzeros;
-  const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep;
+  const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep; I8Gather ga;
 };
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST>
+template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST, int AG = AG_ROWS>
 static int launch_i8(const I8Args& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
-  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
-                     a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep);
+  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST, AG>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+                     a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep, a.ga);
   SAMQ_LAUNCH_CHECK("i8_gemm launch");
   return SAMQ_OK;
 }
@@ -422,8 +454,43 @@ extern "C" int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const vo
   if (cfg <= 0) cfg = i8_pick_cfg(M, N, bfmt);
   SAMQ_REQUIRE(i8_cfg_bn(cfg) > 0 && N % i8_cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "i8_gemm: N not divisible by tile");
   I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
-           I8Epi{a_scale, mid_scale, res_scale, out_scale, R, ldr}};
+           I8Epi{a_scale, mid_scale, res_scale, out_scale, R, ldr, 0}, I8Gather{0, 0, 0}};
   return i8_dispatch(a, bfmt, epilogue, cfg, stream);
+}
+
+extern "C" int samq_w8a8_conv_gemm(const int8_t* x, int mode, int B, int Cin, int side, const int8_t* wpacked,
+                                   const float* wscale, const float* bias, void* C, const int8_t* R, int rmod,
+                                   int N, int epilogue, float a_scale, float mid_scale, float res_scale,
+                                   float out_scale, hipStream_t stream) {
+  SAMQ_REQUIRE(x && wpacked && wscale && C, SAMQ_ERR_INVALID, "w8a8_conv_gemm: null pointer");
+  SAMQ_REQUIRE(mode == AG_PATCH || mode == AG_3X3, SAMQ_ERR_INVALID, "w8a8_conv_gemm: mode must be 1 (patch) or 2 (3x3)");
+  SAMQ_REQUIRE(epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_RES, SAMQ_ERR_UNSUPPORTED,
+               "w8a8_conv_gemm: epilogue must be Q8 or Q8_RES");
+  SAMQ_REQUIRE(B > 0 && Cin > 0 && side > 0 && N > 0 && N % 64 == 0, SAMQ_ERR_INVALID, "w8a8_conv_gemm: bad shape");
+  SAMQ_REQUIRE(out_scale > 0.f, SAMQ_ERR_INVALID, "w8a8_conv_gemm: needs out_scale > 0");
+  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES || (R && ((uintptr_t)R & 15) == 0), SAMQ_ERR_INVALID,
+               "w8a8_conv_gemm: Q8_RES needs a 16-byte aligned residual");
+  SAMQ_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)C & 15) == 0, SAMQ_ERR_INVALID,
+               "w8a8_conv_gemm: operands must be 16-byte aligned");
+  int G, K;
+  if (mode == AG_PATCH) {
+    SAMQ_REQUIRE(side % 16 == 0 && (Cin * 256) % 128 == 0, SAMQ_ERR_UNSUPPORTED,
+                 "w8a8_conv_gemm: patch mode is the 16x16 / stride 16 PatchEmbed");
+    G = side / 16;
+    K = Cin * 256;
+  } else {
+    SAMQ_REQUIRE(Cin % 128 == 0, SAMQ_ERR_UNSUPPORTED, "w8a8_conv_gemm: 3x3 mode needs Cin % 128 == 0");
+    G = side;
+    K = 9 * Cin;
+  }
+  const int M = B * G * G;
+  I8Args a{x, K, (const char*)wpacked, wscale, nullptr, bias, C, N, M, N, K,
+           I8Epi{a_scale, mid_scale, res_scale, out_scale, R, N, rmod}, I8Gather{side, G, Cin}};
+  if (epilogue == SAMQ_EPI_Q8)
+    return mode == AG_PATCH ? launch_i8<64, 64, 2, 2, SAMQ_EPI_Q8, BF_W8, 3, AG_PATCH>(a, stream)
+                            : launch_i8<64, 64, 2, 2, SAMQ_EPI_Q8, BF_W8, 3, AG_3X3>(a, stream);
+  return mode == AG_PATCH ? launch_i8<64, 64, 2, 2, SAMQ_EPI_Q8_RES, BF_W8, 3, AG_PATCH>(a, stream)
+                          : launch_i8<64, 64, 2, 2, SAMQ_EPI_Q8_RES, BF_W8, 3, AG_3X3>(a, stream);
 }
 
 extern "C" int samq_w8a8_gemm(const int8_t* A, int64_t lda, const int8_t* wpacked, const float* wscale,

@@ -685,9 +685,11 @@ class W8A8Engine:
       use_rel_pos_qact, softmax, attn.qact2) -> int8 | proj GEMM + attn.qact3 + residual +
       blk.qact2 -> int8 x | LN2+qact3 -> int8 | lin1 GEMM + GELU + mlp.qact1 -> int8 |
       lin2 GEMM + mlp.qact2 + residual + blk.qact4 -> int8 x.
-    Patch embed: image quantiser (HIP) + im2col (index copy) + GEMM whose epilogue applies
-    patch_embed.qact, adds qact_pos(pos_embed) and applies qact1.  Neck: 1x1 GEMM + qacts.0,
-    LN2d + qacts.1, 3x3 GEMM (im2col of codes) + qacts.2, LN2d + qacts.3 -> f32.
+    Patch embed: image quantiser (HIP) + an implicit GEMM gathering the 16x16 patches from the
+    NCHW codes (``samq_w8a8_conv_gemm`` mode 1) whose epilogue applies patch_embed.qact, adds
+    qact_pos(pos_embed) and applies qact1.  Neck: 1x1 GEMM + qacts.0, LN2d + qacts.1, 3x3 implicit
+    GEMM over the NHWC codes with the zero padding in the gather (mode 2) + qacts.2, LN2d +
+    qacts.3 -> f32.  No im2col / pad copies.
     """
 
     def __init__(self, enc: ImageEncoderViT):
@@ -730,19 +732,20 @@ class W8A8Engine:
                 s_ao=_s(a.qact2), s_proj=_s(a.qact3), s_x1=_s(blk.qact2), s_ln2=_s(blk.qact3),
                 s_h=_s(blk.mlp.qact1), s_l2=_s(blk.mlp.qact2), s_x2=_s(blk.qact4)))
         self.neck0 = self._weight(enc.neck[0])
-        self.neck2 = self._weight(enc.neck[2])
+        self.neck2 = self._weight(enc.neck[2], tap_major=True)
         self.ln_n1 = (enc.neck[1].weight.detach().float().contiguous(), enc.neck[1].bias.detach().float().contiguous(),
                       enc.neck[1].eps)
         self.ln_n3 = (enc.neck[3].weight.detach().float().contiguous(), enc.neck[3].bias.detach().float().contiguous(),
                       enc.neck[3].eps)
         self.s_q = [_s(q) for q in enc.qacts]
 
-    def _weight(self, mod):
+    def _weight(self, mod, tap_major: bool = False):
         """Per-output-channel symmetric int8 codes of a QLinear / QConv2d weight (the reference's
-        ``quantizer(self.weight)``, layers.py:196-199) packed for the int8 MFMA GEMM."""
+        ``quantizer(self.weight)``, layers.py:196-199) packed for the int8 MFMA GEMM.
+        ``tap_major``: conv weight flattened (n, ky, kx, c), the implicit 3x3 GEMM's K order."""
         w = mod.weight.detach().float()
         n = w.shape[0]
-        w2 = w.reshape(n, -1)
+        w2 = (w.permute(0, 2, 3, 1) if tap_major else w).reshape(n, -1)
         s = mod.quantizer.scale
         if s is None:
             raise RuntimeError("fq_vit: weight quantizer is not calibrated")
@@ -771,10 +774,16 @@ class W8A8Engine:
         gh, gw = hh // p, ww // p
         c = self.embed_dim
         codes = ops.quantize(img, self.s_in)
-        cols = codes.view(b, cin, gh, p, gw, p).permute(0, 2, 4, 1, 3, 5).reshape(b * gh * gw, cin * p * p)
-        pos = self.pos_codes if b == 1 else self.pos_codes.repeat(b, 1)
-        x = self._gemm(cols.contiguous(), self.patch_w, ops.EPI_Q8_RES, self.s_in, self.s_x0, mid=self.s_pe, res=pos,
-                       res_scale=self.s_pos)
+        if p == 16 and hh == ww:
+            pw = self.patch_w
+            x = ops.w8a8_conv_gemm(codes, 1, pw["packed"], pw["scale"], pw["n"], pw["bias"], ops.EPI_Q8_RES,
+                                   self.s_in, self.s_x0, mid_scale=self.s_pe, res_scale=self.s_pos, res=self.pos_codes,
+                                   rmod=gh * gw).view(b * gh * gw, c)
+        else:   # other patch geometries: explicit im2col
+            cols = codes.view(b, cin, gh, p, gw, p).permute(0, 2, 4, 1, 3, 5).reshape(b * gh * gw, cin * p * p)
+            pos = self.pos_codes if b == 1 else self.pos_codes.repeat(b, 1)
+            x = self._gemm(cols.contiguous(), self.patch_w, ops.EPI_Q8_RES, self.s_in, self.s_x0, mid=self.s_pe,
+                           res=pos, res_scale=self.s_pos)
         s_x = self.s_x0
         tap("qact1", x.view(b, gh, gw, c), s_x)
         xn = torch.empty_like(x)
@@ -806,9 +815,9 @@ class W8A8Engine:
         y0 = self._gemm(x, self.neck0, ops.EPI_Q8, s_x, sq[0])
         y1 = ops.layernorm_q(y0, self.ln_n1[0], self.ln_n1[1], self.ln_n1[2], in_scale=sq[0], out_scale=sq[1])
         oc = y1.shape[-1]
-        pad = F.pad(y1.view(b, gh, gw, oc), (0, 0, 1, 1, 1, 1))
-        cols3 = pad.unfold(1, 3, 1).unfold(2, 3, 1).reshape(b * gh * gw, oc * 9).contiguous()
-        y2 = self._gemm(cols3, self.neck2, ops.EPI_Q8, sq[1], sq[2])
+        n2 = self.neck2
+        y2 = ops.w8a8_conv_gemm(y1.view(b, gh, gw, oc).contiguous(), 2, n2["packed"], n2["scale"], n2["n"], n2["bias"],
+                                ops.EPI_Q8, sq[1], sq[2]).view(b * gh * gw, -1)
         y3 = ops.layernorm_q(y2, self.ln_n3[0], self.ln_n3[1], self.ln_n3[2], in_scale=sq[2], out_scale=sq[3],
                              out_dtype=torch.float32)
         return y3.view(b, gh, gw, oc).permute(0, 3, 1, 2)

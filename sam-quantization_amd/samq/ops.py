@@ -328,6 +328,29 @@ def w8a8_gemm(a, wpacked, wscale, n, bias=None, epilogue=EPI_Q8, a_scale=1.0, ou
                    res_scale, res, out)
 
 
+def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: torch.Tensor, n: int,
+                   bias: Optional[torch.Tensor] = None, epilogue: int = EPI_Q8, a_scale: float = 1.0,
+                   out_scale: float = 0.0, mid_scale: float = 0.0, res_scale: float = 0.0,
+                   res: Optional[torch.Tensor] = None, rmod: int = 0) -> torch.Tensor:
+    """fq_vit QConv2d on int8 codes as an implicit GEMM (``samq_w8a8_conv_gemm``): mode 1 = the
+    16x16 / stride-16 PatchEmbed on NCHW codes (B, Cin, S, S); mode 2 = the 3x3 / pad-1 neck conv on
+    NHWC codes (B, G, G, Cin).  Returns int8 codes (B, G, G, n)."""
+    _need_cuda(x, wpacked, wscale, bias, res)
+    assert x.dtype == torch.int8 and x.is_contiguous() and wscale.dtype == torch.float32
+    if mode == 1:
+        b, cin, side, _ = x.shape
+        g = side // 16
+    else:
+        b, g, _, cin = x.shape
+        side = g
+    out = torch.empty((b, g, g, n), dtype=torch.int8, device=x.device)
+    _lib.check(_lib.load().samq_w8a8_conv_gemm(_ptr(x), mode, b, cin, side, _ptr(wpacked), _ptr(wscale), _ptr(bias),
+                                               _ptr(out), _ptr(res), rmod, n, epilogue, float(a_scale),
+                                               float(mid_scale), float(res_scale), float(out_scale), _stream()),
+               "w8a8_conv_gemm")
+    return out
+
+
 def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_scale=1.0, out_scale=0.0,
               out=None, groupsize=-1):
     """GPTQ int4 weights (repacked layout 3) x int8 activation codes."""

@@ -346,3 +346,45 @@ def test_w8a8_encoder_vs_golden(cuda, golden_dir, tag, img):
     assert ours[1] <= 1.25 * self_[1] + 0.05
     assert ours[3] >= 0.995
     assert ours[2] * s_out <= 0.15 * np.abs(ref).max() * s_out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_w8a8_conv_gemm_implicit_vs_im2col(cuda, mode):
+    """The implicit-GEMM gathers (samq_w8a8_conv_gemm: 16x16 PatchEmbed on NCHW codes, 3x3 pad-1
+    conv on NHWC codes) give exactly the codes of the explicit im2col + samq_w8a8_gemm path
+    (int32-exact sums, same epilogue), incl. the per-image residual row (pos codes, rmod)."""
+    from samq import ops
+    import torch.nn.functional as F
+    g = torch.Generator(device="cpu").manual_seed(30 + mode)
+    b, n = 2, 256
+    if mode == 1:
+        cin, side = 3, 128
+        x = torch.randint(-128, 128, (b, cin, side, side), generator=g, dtype=torch.int8)
+        gg = side // 16
+        cols = x.view(b, cin, gg, 16, gg, 16).permute(0, 2, 4, 1, 3, 5).reshape(b * gg * gg, cin * 256)
+        w = torch.randint(-127, 128, (n, cin * 256), generator=g, dtype=torch.int8)
+        wk = w
+    else:
+        cin, gg = 256, 12
+        x = torch.randint(-128, 128, (b, gg, gg, cin), generator=g, dtype=torch.int8)
+        pad = F.pad(x.float(), (0, 0, 1, 1, 1, 1))
+        cols = pad.unfold(1, 3, 1).unfold(2, 3, 1).reshape(b * gg * gg, cin * 9).to(torch.int8)   # (c, ky, kx)
+        w4 = torch.randint(-127, 128, (n, cin, 3, 3), generator=g, dtype=torch.int8)
+        w = w4.reshape(n, -1)
+        wk = w4.permute(0, 2, 3, 1).reshape(n, -1)    # tap-major for the implicit GEMM
+    ws = (torch.rand(n, generator=g) * 0.01 + 0.001).float().to(cuda)
+    bias = (torch.randn(n, generator=g) * 0.1).float().to(cuda)
+    pos = torch.randint(-128, 128, (gg * gg, n), generator=g, dtype=torch.int8).to(cuda)
+    packed = ops.w8_repack(w.to(cuda).contiguous())
+    packed_k = ops.w8_repack(wk.to(cuda).contiguous())
+    if mode == 1:
+        ref = ops.w8a8_gemm(cols.to(cuda).contiguous(), packed, ws, n, bias, ops.EPI_Q8_RES, 0.02, 0.05, 0.04, 0.03,
+                            pos.repeat(b, 1))
+        out = ops.w8a8_conv_gemm(x.to(cuda).contiguous(), 1, packed_k, ws, n, bias, ops.EPI_Q8_RES, 0.02, 0.05,
+                                 mid_scale=0.04, res_scale=0.03, res=pos, rmod=gg * gg)
+    else:
+        ref = ops.w8a8_gemm(cols.to(cuda).contiguous(), packed, ws, n, bias, ops.EPI_Q8, 0.02, 0.05)
+        out = ops.w8a8_conv_gemm(x.to(cuda).contiguous(), 2, packed_k, ws, n, bias, ops.EPI_Q8, 0.02, 0.05)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(-1, n), ref.view(-1, n))
