@@ -326,7 +326,6 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   __shared__ __attribute__((aligned(16))) _Float16 v_lds[2][KC * VP];
   __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
   __shared__ float rh_lds[NWQ][16 * (G + 1)];
-  __shared__ float rw_lds[NWQ][16 * (G + 1)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -370,41 +369,43 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   load(0);
 
   // ---- this wave's 16 queries (codes) and their rel-pos terms: fp32 dot products of the
-  // fake-quant q with the f32 tables (rows qy - k + 63 for both, quirk 1)
+  // fake-quant q with the f32 tables (rows qy - k + 63 for both, quirk 1).  Lane (g, ql) computes
+  // the terms of query ql at k = 16 bb + 4 g + i: rel_w straight into the registers the score loop
+  // reads, rel_h into LDS (one value per key row per chunk); no rel_w table in LDS, so three
+  // workgroups fit a CU (the 768 workgroups of a vit_b launch are then all resident at once).
   const int4v qfrag = *(const int4v*)(img + ((int64_t)qy * G + qx) * ts + head * QD + g * 16);
   *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
   __builtin_amdgcn_s_waitcnt(0xC07F);
-  for (int pi = lane; pi < 16 * G; pi += 64) {
-    const int qi = pi & 15, kk = pi >> 4;
-    const int ridx = qy - kk + G - 1;
-    const float* th = p.relh + (int64_t)ridx * QD;
-    const float* tw = p.relw + (int64_t)ridx * QD;
-    float ah = 0.f, aw = 0.f;
-#pragma unroll 1
-    for (int d4 = 0; d4 < QD / 16; ++d4) {
-      const u32x4 cw = *(const u32x4*)(&q_lds[wave][qi * KPITCH + d4 * 16]);
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
-        const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
-          ah = fmaf(qf, h4[e], ah);
-          aw = fmaf(qf, w4[e], aw);
-        }
-      }
-    }
-    rh_lds[wave][qi * (G + 1) + kk] = ah;
-    rw_lds[wave][qi * (G + 1) + kk] = aw;
-  }
-  store(0);
-  __syncthreads();   // chunk 0 staged; this wave's rel terms visible to itself
   float rwr[4][4];
 #pragma unroll
   for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) rwr[bb][i] = rw_lds[wave][ql * (G + 1) + bb * 16 + 4 * g + i];
+    for (int i = 0; i < 4; ++i) {
+      const int kk = 16 * bb + 4 * g + i;
+      const int ridx = qy - kk + G - 1;
+      const float* th = p.relh + (int64_t)ridx * QD;
+      const float* tw = p.relw + (int64_t)ridx * QD;
+      float ah = 0.f, aw = 0.f;
+#pragma unroll 1
+      for (int d4 = 0; d4 < QD / 16; ++d4) {
+        const u32x4 cw = *(const u32x4*)(&q_lds[wave][ql * KPITCH + d4 * 16]);
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
+          const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
+            ah = fmaf(qf, h4[e], ah);
+            aw = fmaf(qf, w4[e], aw);
+          }
+        }
+      }
+      rh_lds[wave][ql * (G + 1) + kk] = ah;
+      rwr[bb][i] = aw;
+    }
+  store(0);
+  __syncthreads();   // chunk 0 staged; the rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (G + 1)];
 
   const float c1 = p.qk_scale * p.inv_a1, sa1 = p.s_a1, inv2 = p.inv_a2, k2 = p.k2;
