@@ -45,6 +45,7 @@ struct AttnParams {
   int H, W;                 // image token grid
   int nwx, upi;             // windows per row, windows per image
   float scale;              // sm_scale
+  int nqb, units;           // streaming path with a 1-D XCD-ordered grid: query blocks, units
 };
 
 template <int N>
@@ -99,8 +100,18 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   const int wave = tid >> 6;
   const int ql = lane & 15;
   const int g = lane >> 4;
-  const int head = blockIdx.y;
-  const int unit = blockIdx.z;
+  // XCD-aware order for the streaming (global) path: the grid is 1-D and the query blocks of one
+  // (image, head) all land on one XCD (workgroups are dealt round-robin over the 8 XCDs), so that
+  // XCD's L2 serves their shared K/V stream instead of every XCD fetching every head's keys
+  int qblk = blockIdx.x, head = blockIdx.y, unit = blockIdx.z;
+  if (!RESIDENT && gridDim.y == 1 && gridDim.z == 1) {
+    const int nqb = p.nqb, pairs = p.heads * p.units;
+    const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
+    const int pair = xcd * (pairs >> 3) + k / nqb;
+    qblk = k % nqb;
+    head = pair % p.heads;
+    unit = pair / p.heads;
+  }
   const int S = SC ? SC : p.S;   // grid side, compile-time where the dispatcher knows it
   const int b = unit / p.upi;
   const int wi = unit % p.upi;
@@ -165,7 +176,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   int qrow[QT], qcol0[QT];
 #pragma unroll
   for (int t = 0; t < QT; ++t) {
-    const int qi = (blockIdx.x * NW + wave) * QT + t;
+    const int qi = (qblk * NW + wave) * QT + t;
     qrow[t] = qi / KT;
     qcol0[t] = (qi % KT) * 16;
     const int kind = tok_kind(qrow[t], qcol0[t] + ql);
@@ -808,8 +819,16 @@ template <int D, int SP, int QT, int NW, bool RES, bool PRE, int RS = 16, int SC
 static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
   const int tiles = p.S * (SP / 16);
   const int qblocks = (tiles + NW * QT - 1) / (NW * QT);
-  hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS, SC>), dim3(qblocks, p.heads, units),
-                     dim3(64 * NW), 0, stream, p);
+  if (!RES && (p.heads * units) % 8 == 0) {   // 1-D grid, XCD-aware (see the kernel)
+    AttnParams q = p;
+    q.nqb = qblocks;
+    q.units = units;
+    hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS, SC>), dim3(qblocks * p.heads * units),
+                       dim3(64 * NW), 0, stream, q);
+  } else {
+    hipLaunchKernelGGL((rel_attention_kernel<D, SP, QT, NW, RES, PRE, RS, SC>), dim3(qblocks, p.heads, units),
+                       dim3(64 * NW), 0, stream, p);
+  }
   SAMQ_LAUNCH_CHECK("rel_attention launch");
   return SAMQ_OK;
 }
