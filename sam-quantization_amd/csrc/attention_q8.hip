@@ -39,7 +39,7 @@ struct AttnQ8Params {
 typedef int int4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float aq8(float v, float s) {
-  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);
+  return q8_exact(v, s, 1.0f / s);   // s is a kernel argument: the reciprocal is hoisted
 }
 
 constexpr int QD = 64;       // head dim (vit_b)

@@ -58,6 +58,17 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return 0.5f * x * (1.0f + erf_v);
 }
 
+// clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
+// quantizer/uniform.py:31-36), at the price of a multiply: q = v * inv (inv = fl(1/s)) is within
+// ~1.2e-7 |q| of v / s and fl(v / s) within 6e-8 |q|, so rint(q) == rint(fl(v / s)) unless q lies
+// within 1e-6 max(|q|, 1) of a half-integer -- only then (rare) the true division runs.
+__device__ __forceinline__ float q8_exact(float v, float s, float inv) {
+  const float q = v * inv;
+  float r = __builtin_rintf(q);
+  if (fabsf(q - r) > 0.5f - 1e-6f * fmaxf(fabsf(q), 1.0f)) r = __builtin_rintf(v / s);
+  return fminf(fmaxf(r, -128.f), 127.f);
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

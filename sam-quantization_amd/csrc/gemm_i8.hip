@@ -44,10 +44,6 @@ enum { AG_ROWS = 0, AG_PATCH = 1, AG_3X3 = 2 };
 struct I8Gather { int S, G, Cin; };
 __device__ __attribute__((aligned(16))) int8_t g_zero_i8[16];
 
-__device__ __forceinline__ float q8f(float v, float s) {
-  // clamp(round_half_even(v / s), -128, 127)   (quantizer/uniform.py:31-36, true division)
-  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);
-}
 
 template <int N>
 __device__ __forceinline__ void vm_wait_i8() {
@@ -262,6 +258,8 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   const int row_base = m0 + wm * WM;
   const int col_base = n0 + wn * WN;
   constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
+  const float inv_out = ep_args.out_scale > 0.f ? 1.0f / ep_args.out_scale : 0.f;   // q8_exact (common.h)
+  const float inv_mid = ep_args.mid_scale > 0.f ? 1.0f / ep_args.mid_scale : 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -332,11 +330,11 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
               for (int b = 0; b < 4; ++b) {
                 float x = v[4 * w + b];
                 if (EPI == SAMQ_EPI_Q8_RES) {
-                  if (ep_args.mid_scale > 0.f) x = q8f(x, ep_args.mid_scale) * ep_args.mid_scale;
+                  if (ep_args.mid_scale > 0.f) x = q8_exact(x, ep_args.mid_scale, inv_mid) * ep_args.mid_scale;
                   const float rv = (float)(int8_t)((res[w] >> (8 * b)) & 0xFFu) * ep_args.res_scale;
                   x = rv + x;
                 }
-                const int qv = (int)q8f(x, ep_args.out_scale);
+                const int qv = (int)q8_exact(x, ep_args.out_scale, inv_out);
                 word |= ((uint32_t)qv & 0xFFu) << (8 * b);
               }
               o[w] = word;

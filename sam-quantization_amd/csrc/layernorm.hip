@@ -10,8 +10,8 @@ namespace samq {
 // OUT: 0 f16, 1 f32, 2 int8 codes q(y, out_scale), 3 f32 fake-quant q(y, out_scale) * out_scale
 enum { LN_F32 = 0, LN_F16 = 1, LN_I8 = 2, LN_FQ32 = 3 };
 
-__device__ __forceinline__ float ln_q8(float v, float s) {
-  return fminf(fmaxf(__builtin_rintf(v / s), -128.f), 127.f);   // fq_vit uniform.py:31-36
+__device__ __forceinline__ float ln_q8(float v, float s) {   // fq_vit uniform.py:31-36
+  return q8_exact(v, s, 1.0f / s);   // the reciprocal is loop-invariant (hoisted)
 }
 
 template <int IN, int OUT, int VPT, int RPW>  // VPT = 4-channel vectors per lane, RPW = rows per wave

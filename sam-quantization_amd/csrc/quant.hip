@@ -1,7 +1,7 @@
 // Elementwise activation quantiser: fq_vit QAct in quant mode (fq_vit/models/ptq/layers.py:232-242
 // -> BaseQuantizer.forward, quantizer/base.py:43-49 -> UniformQuantizer.quant/dequantize,
 // quantizer/uniform.py:23-45) with the int8 symmetric layer-wise configuration (zero point 0):
-//   code = clamp(round_half_even(x / s), -128, 127)   (true division, as the reference)
+//   code = clamp(round_half_even(x / s), -128, 127)   (the correctly rounded quotient, via q8_exact)
 // Output int8 codes (consumed by the int8 GEMMs / attention) or the f32 fake-quant value.
 // HBM-bound: 4 elements per lane per step, grid-stride.
 #include "common.h"
@@ -11,6 +11,7 @@ namespace samq {
 template <bool IN_F16, bool OUT_FQ>
 __global__ __launch_bounds__(256) void quantize_kernel(const void* __restrict__ x, void* __restrict__ y, int64_t n,
                                                        float s) {
+  const float inv = 1.0f / s;   // q8_exact (common.h): multiply, true division only near ties
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4 + (n & 3); i += stride) {
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(256) void quantize_kernel(const void* __restrict__ 
     }
     float q[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) q[e] = fminf(fmaxf(__builtin_rintf(v[e] / s), -128.f), 127.f);
+    for (int e = 0; e < 4; ++e) q[e] = q8_exact(v[e], s, inv);
     if (OUT_FQ) {
       if (cnt == 4) ((float4_t*)y)[i] = float4_t{q[0] * s, q[1] * s, q[2] * s, q[3] * s};
       else ((float*)y)[base] = q[0] * s;

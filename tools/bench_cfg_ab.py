@@ -1,0 +1,47 @@
+"""Interleaved A/B of per-layer W4A16 tile configs INSIDE the timed HIP graph (ViT-H, B=4):
+each variant is captured once and the graphs are replayed in rounds A B C A B C ... so box drift
+hits every variant alike.  usage: python tools/bench_cfg_ab.py [lanes] [rounds]"""
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "sam-quantization_amd"))
+from samq.synthetic import random_quant_encoder  # noqa: E402
+
+dev = torch.device("cuda:0")
+lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+VARIANTS = {"pick": {}, "lin1=22": {"lin1": 22}, "qkv=56": {"qkv": 56}, "lin1=22,qkv=22": {"lin1": 22, "qkv": 22}}
+
+enc = random_quant_encoder("vit_h", -1, device=dev)
+eng = enc.engine()
+g = torch.Generator(device=dev).manual_seed(1234)
+img = torch.randn((4, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
+graphs, ref = {}, None
+for name, cfg in VARIANTS.items():
+    for p in eng.plans:
+        for lay in ("qkv", "proj", "lin1", "lin2"):
+            getattr(p, lay).gemm_cfg = cfg.get(lay, 0)
+    graph, out = eng.capture(img, lanes=lanes)
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = out.clone() if ref is None else ref
+    graphs[name] = (graph, torch.equal(out, ref))
+times = {k: [] for k in graphs}
+for _ in range(rounds):
+    for name, (graph, _) in graphs.items():
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(10):
+            graph.replay()
+        torch.cuda.synchronize()
+        times[name].append((time.perf_counter() - t) / 10 * 1e3)
+for name, ts in times.items():
+    ts.sort()
+    print(f"lanes={lanes} {name:16s} median {ts[len(ts) // 2]:.3f} ms/step  min {ts[0]:.3f}  "
+          f"({4 / ts[len(ts) // 2] * 1e3:.1f} img/s)  bit-identical: {graphs[name][1]}", flush=True)

@@ -44,7 +44,8 @@ def main():
         fake, s, z = rtn(w)
         pack_linear(q, fake, s, z, torch.randn(n, device=dev) * 0.02)
         packed = q.prepare()
-        packed2 = ops.w4_repack(q.qweight, layout=2)
+        # layout-2 weights exist only in the tuning build (SAMQ_LIB=tuning, make tuning)
+        packed2 = ops.w4_repack(q.qweight, layout=2) if any(40 <= c < 50 for c in cfgs) else None
         pk = lambda c: packed2 if 40 <= c < 50 else packed  # noqa: E731
         a = torch.randn(m, k, device=dev).half()
         f32 = epi in (ops.EPI_RESADD_F32, ops.EPI_F32)

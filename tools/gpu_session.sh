@@ -29,6 +29,8 @@ for step in "$@"; do
     bench)   run bench 500 python bench.py --steps 20 --warmup 5 ;;
     bench48) run bench_w4a8 600 python bench.py --mode w4a8 --steps 10 --warmup 3 ;;
     bench88) run bench_w8a8 600 python bench.py --mode w8a8 --steps 20 --warmup 5 ;;
+    b48q)    run b48q 400 python bench.py --mode w4a8 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    b88q)    run b88q 400 python bench.py --mode w8a8 --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     instep)  run instep 500 bash tools/instep_profile.sh w4a16 ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
