@@ -27,9 +27,19 @@
 //    query of the wave raised its max (alpha == 1 exactly, bit-identical results).
 #include "common.h"
 
+#include <type_traits>
+
 namespace samq {
 
 constexpr float LOG2E = 1.4426950408889634f;
+
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {   // f(integral_constant<int, 0..N-1>)
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
 
 __device__ __attribute__((aligned(16))) _Float16 g_zero16[8];   // zero source for pad slots
 
@@ -64,6 +74,14 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 __device__ __forceinline__ half4_t ds_read_tr16(uint32_t addr) {
   half4_t r;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+template <int OFF>   // same, with the instruction's 16-bit immediate offset (no VGPR per address)
+__device__ __forceinline__ half4_t ds_read_tr16_off(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  half4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
   return r;
 }
 
@@ -461,260 +479,233 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   }
 }
 
-// ------------------------------------------------------------------ windowed attention, persistent
-// The 14x14-window blocks (28 of 32 in ViT-H) as a persistent kernel: one workgroup per CU walks
-// its share of the (window, head) items with the NEXT item's K/V already streaming into the
-// second LDS buffer (LDS-DMA) and its Q into registers while the current item computes, so the
-// HBM stream and the MFMA/VALU work overlap inside one CU.  Per item, everything is local to
-// the window and the VALU work per score is cut to max3/sub/exp/cvt:
-//  * the whole score s[q,k] = q.k*scale + TH[q,kh] + TW[q,kw] (log2 domain) comes out of the
-//    MFMAs: S^T = K'.Q'^T on 16x16x32 with TW as the C input, and TH carried by 16 extra
-//    contraction dims -- K' rows get a one-hot of their key row (DMA'd from a constant table
-//    next to the K data), Q' rows get TH[q, 0..15] in fp16 (the reference also rounds rel_h to
-//    fp16, fused_attention.py:46-80); for D = 80 these are the zero-padded dims 80..95 of the
-//    third k-step, so TH costs no MFMA at all;
-//  * one exact softmax over the window's 196 keys (no online rescale); the two masked slots of
-//    each 16-slot key row are -inf in the C input;
-//  * O^T += V^T . P^T on 16x16x32 with two key rows per MFMA (k order [row 2p: 4g..4g+3 |
-//    row 2p+1: 4g..4g+3], the score registers' own layout; V^T by ds_read_b64_tr_b16), and the
-//    softmax denominator as one more MFMA against an all-ones A operand (sum of the same fp16
-//    P that multiplies V);
-//  * the rel-pos tables (shared by every window and head) sit in LDS for the whole kernel.
-// Items are numbered so the 32 workgroups of one XCD take the 16 heads of the same two windows
-// at a time (the cache lines shared by adjacent heads' K/V slices then land in one L2).
-struct OneHot16 { uint16_t v[16 * 16]; };
-constexpr OneHot16 make_onehot16() {
-  OneHot16 o{};
-  for (int r = 0; r < 16; ++r) o.v[r * 16 + r] = 0x3C00;   // fp16 1.0 on the diagonal
-  return o;
-}
-__device__ __attribute__((aligned(16))) OneHot16 g_onehot16 = make_onehot16();
-
+// ------------------------------------------------------------------ windowed attention (14 x 14)
+// The 14x14-window blocks (28 of 32 in ViT-H).  One (window, head) item per 4-wave workgroup, TWO
+// workgroups per CU (LDS < 80 KiB, <= 256 VGPRs): the partner workgroup runs out of phase, so
+// one's HBM wait, softmax VALU and MFMA runs overlap the other's (no barrier couples them), and the
+// hardware deals the 800 items of a 2-image ViT-H launch dynamically over the 512 slots.
+//  * LDS image of an item: per key row kh (16 key slots; slots 14, 15 duplicate slot 13 and are
+//    masked) NPC 1-KiB pieces, each written by ONE global_load_lds_dwordx4 whose lanes pick their
+//    own sources:  K piece s: position l = (g, ql) holds key ql, dims 32 s + 8 g  -- read back by
+//    lane l itself (ds_read_b128 at l * 16: the A operand of k-step s, conflict-free);  V piece:
+//    position (g8, slot ^ 8 (g8 & 1)) holds key slot, dims 32 dblk + 8 g8 -- the XOR spreads the
+//    ds_read_b64_tr_b16 reads of V^T over all 64 banks.  (D = 80: K dims 64..79 and V dims 64..79
+//    share one piece; lanes of k-step 2 past dim 79 read V bytes against zero Q dims.)
+//    Sources are one 64-bit add per piece (row stride); window pad tokens (past the image) read
+//    the qkv bias, as the reference's zero-padded tokens do after the qkv Linear.
+//  * query rows in passes of two 16-slot tiles per wave (rows 2w, 2w+1 then 8+2w, 9+2w); per tile
+//    TW[q, kw] = q . Rw[qh - kw + 13] and TH[q, kh] = q . Rh[qh - kh + 13] (both indexed by the
+//    query ROW qh: reference quirk 1) come out of 2 x KS MFMAs in the score layout; TW is the C
+//    input of every key row's Q.K^T, TH[q, kh] is added to it per row (lane-local after one LDS
+//    exchange; TH is rounded to fp16 as the reference's rel_h is);
+//  * S^T = K.Q^T per key row (16 x 16 tile, each lane owns one query), one exact softmax over the
+//    window's keys in the exp2 domain, O^T += V^T.P^T two key rows per MFMA with P^T in the score
+//    registers' own k order, the row sum as one more MFMA against ones.
+#ifndef SAMQ_WIN_PREFETCH
+#define SAMQ_WIN_PREFETCH 0
+#endif
 template <int D>
-__global__ __launch_bounds__(64 * 7, 1) void win_attention_kernel(AttnParams p, int items) {
-  constexpr int S = 14, NW = 7, QT = 2;
-  constexpr int KS = 3;                         // k32 steps of Q'.K'^T: D + 16 TH dims <= 96
-  constexpr int DT = D / 16;
-  constexpr int D8 = D / 8;
-  constexpr int KCH = D8 + 2;                   // 16-byte chunks per K' row (data + one-hot)
-  constexpr int KROW = KCH * 16;                // K' row pitch (bytes)
-  constexpr int GTH = (D - 64) / 8;             // first lane group holding TH dims in k-step 2
-  constexpr int RKEYS = S * S + 16 - S;         // 196 keys + slack for the last row's 16-slot tile
-  constexpr int KC = RKEYS * KCH, VC = RKEYS * D8;
-  constexpr int NI = (KC + VC + 64 * NW - 1) / (64 * NW);
-  constexpr int BUFB = NI * NW * 1024;
-  constexpr int TAB = (2 * S - 1) * D;          // elements per rel-pos table
-  constexpr int TABP = TAB + 32;                // + slack: k-step-2 reads past the last row
-  constexpr int TH16_BYTES = NW * QT * 16 * 32;
-  constexpr int SMEM = 2 * TABP * 2 + TH16_BYTES + 2 * BUFB;
-  static_assert(SMEM <= 160 * 1024, "LDS");
+__global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int items) {
+  constexpr int S = 14, QT = 2;
+  constexpr int KS = D == 80 ? 3 : 2;            // k32 steps of Q.K^T
+  constexpr int DT = D / 16;                     // output d tiles
+  constexpr int NPC = D == 80 ? 5 : 4;           // 1-KiB pieces per key row
+  constexpr int ROWB = NPC * 1024;
+  constexpr int V0 = (NPC - 2) * 1024;           // V dims 0..31 piece (dims 32..63 follow)
+  constexpr int THB = 4 * QT * 16 * 32;          // TH exchange [wave][t][query][16 kh] fp16
+  constexpr int SMEM = S * ROWB + THB;
+  static_assert(SMEM <= 80 * 1024, "two workgroups per CU");
   static_assert(D == 64 || D == 80, "head dim");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  _Float16* tab_h = (_Float16*)smem;
-  _Float16* tab_w = tab_h + TABP;
-  char* th16 = smem + 2 * TABP * 2;
-  char* bufs = th16 + TH16_BYTES;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int ql = lane & 15;
   const int g = lane >> 4;
+  // consecutive items (the heads of one window: K/V cache lines shared across head slices) on one XCD
+  const int item = xcd_remap(blockIdx.x, gridDim.x);
+  if (item >= items) return;
+  const int unit = item / p.heads;
+  const int head = item - unit * p.heads;
+  const int b = unit / p.upi;
+  const int wi = unit - b * p.upi;
+  const int wy = wi / p.nwx;
+  const int Y0 = wy * S, X0 = (wi - wy * p.nwx) * S;
+  const int nrow = p.H - Y0 < S ? p.H - Y0 : S;  // rows / columns of the window inside the image
+  const int ncol = p.W - X0 < S ? p.W - X0 : S;
   const int C = p.C;
   const int64_t ts = p.tok_stride;
+  const int64_t rowstride = (int64_t)p.W * ts;
+  const _Float16* tok0 = p.qkv + (((int64_t)b * p.H + Y0) * p.W + X0) * ts;
   const float qscale = p.scale * LOG2E;
-  const bool qin2 = 64 + 8 * g < D;             // lane holds real q dims in k-step 2
-  const bool thl = g == GTH || g == GTH + 1;    // lane holds TH dims in k-step 2
+  const float inv_scale = 1.0f / p.scale;        // (Qs . R) / scale = log2e * (q . R)
 
-  // rel-pos tables -> LDS (once per workgroup); the slack is zeroed
-  for (int i = tid; i < 2 * TABP / 8; i += 64 * NW) {
-    const int which = i >= TABP / 8;
-    const int j = which ? i - TABP / 8 : i;
-    half8_t v = {};
-    if (8 * j < TAB) v = *(const half8_t*)((which ? p.relw : p.relh) + 8 * j);
-    *(half8_t*)((which ? tab_w : tab_h) + 8 * j) = v;
-  }
-
-  // logical item -> (unit, head); workgroups of one XCD share windows (see header)
-  const int nxcd_wg = gridDim.x >> 3;           // grid is a multiple of 8
-  auto item_of = [&](int it) -> int {
-    const int b = blockIdx.x;
-    return it * gridDim.x + (b & 7) * nxcd_wg + (b >> 3);
-  };
-  struct Geo { int b, Y0, X0, head; bool edge; };
-  auto geo = [&](int item) -> Geo {
-    const int unit = item / p.heads;
-    Geo o;
-    o.head = item - unit * p.heads;
-    o.b = unit / p.upi;
-    const int wi = unit - o.b * p.upi;
-    o.Y0 = (wi / p.nwx) * S;
-    o.X0 = (wi % p.nwx) * S;
-    o.edge = o.Y0 + S > p.H || o.X0 + S > p.W;
-    return o;
-  };
-
-  // ---- per-lane DMA chunk table (item-invariant): offset of the chunk relative to the item's
-  // first token (elements) for token chunks, or into g_onehot16; kind in the top bits
-  // (0 token K/V data, 1 one-hot, 2 zero).  Edge windows re-derive (row, slot) on a slow path.
-  uint32_t chunk[NI];
+  // ---------------------------------------------------------------- K/V -> LDS (one wave per row)
+  {
+    const _Float16* src[NPC];
+    int64_t step[NPC];
+    const _Float16* pad[NPC];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int c = (wave * NI + i) * 64 + lane;
-    const bool isv = c >= KC;
-    const int cc = isv ? c - KC : c;
-    const int per = isv ? D8 : KCH;
-    const int key = cc / per, d8 = cc - (cc / per) * per;
-    const int r = key / S, slot = key - (key / S) * S;
-    uint32_t e;
-    if (c >= KC + VC) e = 2u << 30;
-    else if (!isv && d8 >= D8) e = (1u << 30) | (uint32_t)((r < S ? r : 15) * 16 + 8 * (d8 - D8));
-    else if (r >= S) e = 2u << 30;
-    else e = (uint32_t)((r * p.W + slot) * ts + (isv ? 2 * C : C) + d8 * 8);
-    chunk[i] = e;
-  }
-  auto issue = [&](const Geo& q, int buf) {
-    const _Float16* tok0 = p.qkv + (((int64_t)q.b * p.H + q.Y0) * p.W + q.X0) * ts + q.head * D;
-    const _Float16* onehot = (const _Float16*)&g_onehot16;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      uint32_t e = chunk[i];
-      asm volatile("" : "+v"(e));   // no loop-invariant 64-bit pointers hoisted out of the item loop
-      const uint32_t kind = e >> 30, off = e & 0x3FFFFFFFu;
-      const _Float16* src = kind == 0 ? tok0 + off : (kind == 1 ? onehot + off : g_zero16);
-      if (q.edge && kind == 0) {   // pad token of an edge window: its K/V = the qkv bias
-        const int c = (wave * NI + i) * 64 + lane;
-        const bool isv = c >= KC;
-        const int cc = isv ? c - KC : c;
-        const int per = isv ? D8 : KCH;
-        const int key = cc / per, d8 = cc - (cc / per) * per;
-        const int r = key / S, slot = key - (key / S) * S;
-        if (q.Y0 + r >= p.H || q.X0 + slot >= p.W)
-          src = p.qkv_bias ? p.qkv_bias + (isv ? 2 * C : C) + q.head * D + d8 * 8 : g_zero16;
+    for (int j = 0; j < NPC; ++j) {
+      int col, ch;
+      if (j < KS - (D == 80 ? 1 : 0) || (D == 80 && j == 2 && lane < 32)) {   // K: (g, ql)
+        col = ql;
+        ch = C + head * D + 32 * j + 8 * g;
+      } else {                                                                // V: (g8, slot ^ 8 (g8 & 1))
+        const bool comb = D == 80 && j == 2;      // upper half of the shared K/V piece
+        const int g8 = comb ? g - 2 : g;
+        const int dblk = comb ? 2 : j - (NPC - 2);
+        col = ql ^ (8 * (g8 & 1));
+        ch = 2 * C + head * D + 32 * dblk + 8 * g8;
       }
-      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)src,
-                                       (SAMQ_LDS void*)(bufs + buf * BUFB + (wave * NI + i) * 1024), 16, 0, 0);
+      col = col < S - 1 ? col : S - 1;
+      pad[j] = p.qkv_bias ? p.qkv_bias + ch : g_zero16;
+      const bool real = col < ncol;
+      src[j] = real ? tok0 + (int64_t)col * ts + ch + wave * rowstride : pad[j];
+      step[j] = real ? 4 * rowstride : 0;
+    }
+    for (int kh = wave; kh < S; kh += 4) {
+      const bool rowreal = kh < nrow;
+#pragma unroll
+      for (int j = 0; j < NPC; ++j) {
+        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(rowreal ? src[j] : pad[j]),
+                                         (SAMQ_LDS void*)(smem + kh * ROWB + j * 1024), 16, 0, 0);
+        src[j] += step[j];
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- per-pass operands
+  // raw Q of the tile's 16 query slots (dims 32 s + 8 g; zero past D and for slots 14, 15) and
+  // the rel-pos table fragments of its query row (A operands: row i = key column / key row)
+  auto load_q = [&](int r, half8_t (&q)[KS]) {
+    const bool inwin = ql < S;
+    const bool real = inwin && r < nrow && ql < ncol;
+    const _Float16* base = real ? tok0 + ((int64_t)r * p.W + ql) * ts + head * D
+                                : ((inwin && p.qkv_bias) ? p.qkv_bias + head * D : nullptr);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const _Float16* a = (base && 32 * s + 8 * g < D) ? base + 32 * s + 8 * g : g_zero16;
+      asm volatile("" : "+v"(a));
+      q[s] = *(const SAMQ_GLOBAL half8_t*)a;
     }
   };
-  // Q of this wave's tiles (query row wave*QT + t, slots ql) -> registers, unscaled; every lane
-  // issues every load (zero source for absent data) so the vmcnt count is wave-uniform
-  auto load_q = [&](const Geo& q, half8_t (&qv)[QT][KS]) {
+  auto load_rel = [&](int r, half8_t (&rh)[KS], half8_t (&rw)[KS]) {
+    int idx = r - ql + S - 1;
+    idx = idx < 0 ? 0 : idx;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      int dd = 32 * s + 8 * g;
+      dd = dd < D ? dd : dd - 16;                 // k-step-2 lanes past D: any in-bounds row bytes
+      rh[s] = *(const SAMQ_GLOBAL half8_t*)(p.relh + idx * D + dd);
+      rw[s] = *(const SAMQ_GLOBAL half8_t*)(p.relw + idx * D + dd);
+    }
+  };
+
+  const int npass = 8 + 2 * wave < S ? 2 : 1;
+  half8_t qraw[QT][KS], relh[QT][KS], relw[QT][KS];
+#pragma unroll
+  for (int t = 0; t < QT; ++t) {
+    load_q(2 * wave + t, qraw[t]);
+    load_rel(2 * wave + t, relh[t], relw[t]);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();   // the item's K/V image is complete
+
+  char* thx = smem + S * ROWB + wave * (QT * 16 * 32);
+  // V^T fragment address of this lane (ds_read_b64_tr_b16: lane 4q+p of a group reads key slot
+  // 4g + q, dims 4p..4p+3 of the tile's 16)
+  const int tq = ql >> 2, tp = ql & 3;
+  const int vslot = 4 * g + tq;
+  const uint32_t vlane = lds_addr(smem) + (((tp >> 1) * 16 + (vslot ^ (8 * (tp >> 1)))) * 16 + (tp & 1) * 8);
+  const uint32_t klane = lds_addr(smem) + lane * 16;
+  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
+
+  for (int pass = 0; pass < npass; ++pass) {
+    const int row0 = 8 * pass + 2 * wave;
+    if (!SAMQ_WIN_PREFETCH && pass > 0) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        load_q(row0 + t, qraw[t]);
+        load_rel(row0 + t, relh[t], relw[t]);
+      }
+    }
+    // ---- Q scale (fp16(q * scale * log2e), the reference's rounding) and rel-pos terms
+    half8_t qf[QT][KS];
+    float4_t tw[QT];
+    half8_t th[QT][2];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      const int qr = wave * QT + t;
-      const bool inwin = qr < S && ql < S;
-      const bool real = inwin && q.Y0 + qr < p.H && q.X0 + ql < p.W;
-      const int64_t tok = ((int64_t)q.b * p.H + (q.Y0 + qr)) * p.W + (q.X0 + ql);
-      const _Float16* pad = (inwin && p.qkv_bias) ? p.qkv_bias + q.head * D : nullptr;
-      const _Float16* src = real ? p.qkv + tok * ts + q.head * D : pad;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        const _Float16* a = (src && (s < 2 || qin2)) ? src + 32 * s + 8 * g : g_zero16;
-        asm volatile("" : "+v"(a));   // opaque: keeps the compiler from splitting the loads by source
-        qv[t][s] = *(const SAMQ_GLOBAL half8_t*)a;
-      }
-    }
-  };
-
-  int it = 0;
-  int item = item_of(0);
-  if (item >= items) return;
-  Geo cur = geo(item);
-  half8_t qn[QT][KS];
-  issue(cur, 0);
-  load_q(cur, qn);
-
-  const int trow = ql >> 2;            // ds_read_b64_tr_b16 addressing (see rel_attention_kernel)
-  const int tcol = 4 * (ql & 3);
-  char* th_w = th16 + wave * (QT * 16 * 32);
-  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
-  int buf = 0;
-
-  for (;;) {
-    wait_vmcnt<0>();
-    __syncthreads();   // item's K/V + Q landed and visible; the other buffer is free (all waves past it)
-    half8_t qf[QT][KS];
-#pragma unroll
-    for (int t = 0; t < QT; ++t)
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        half8_t v = qn[t][s];
+        half8_t v = qraw[t][s];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * qscale);
         qf[t][s] = v;
       }
-    const int nitem = item_of(it + 1);
-    const bool has_next = nitem < items;
-    Geo nxt = cur;
-    if (has_next) {
-      nxt = geo(nitem);
-      issue(nxt, buf ^ 1);
-      load_q(nxt, qn);
+      float4_t a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        a = __builtin_amdgcn_mfma_f32_16x16x32_f16(relw[t][s], qf[t][s], a, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(relh[t][s], qf[t][s], c, 0, 0, 0);
+      }
+      a = a * inv_scale;
+      c = c * inv_scale;
+      if (g == 3) { a[2] = -INFINITY; a[3] = -INFINITY; }   // key slots 14, 15
+      tw[t] = a;
+      // lane (g, ql) holds TH[kh = 4g..4g+3][query ql] -> [query][kh] row of this tile
+      *(half4_t*)(thx + (t * 16 + ql) * 32 + 8 * g) = half4_t{(_Float16)c[0], (_Float16)c[1], (_Float16)c[2], (_Float16)c[3]};
     }
-
-    // ---- rel-pos terms: TW -> C input (slots >= S masked to -inf); TH -> the Q' extra dims
-    float4_t tw[QT];
-    const float inv_scale = 1.0f / p.scale;    // (Qs . R) / scale = log2e * (q . R)
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      const int qr = wave * QT + t;
-      const int qh = qr < S ? qr : S - 1;
-      int r = qh - ql + S - 1;
-      r = r < 0 ? 0 : r;
-      float4_t th, tww;
-#pragma unroll
-      for (int which = 0; which < 2; ++which) {
-        const _Float16* rp = (which ? tab_w : tab_h) + r * D;
-        float4_t a = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < KS; ++s)   // k-step 2 of lanes without q dims multiplies zeros
-          a = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const half8_t*)(rp + 32 * s + 8 * g), qf[t][s], a, 0, 0, 0);
-        a = a * inv_scale;
-        if (which) tww = a; else th = a;
-      }
-      if (g == 3) { tww[2] = -INFINITY; tww[3] = -INFINITY; }   // key slots 14, 15
-      tw[t] = tww;
-      // lane (g, ql) holds TH[kh = 4g..4g+3][ql]; lanes of groups GTH, GTH+1 need kh 0..7 / 8..15
-      *(half4_t*)(th_w + (t * 16 + ql) * 32 + 8 * g) =
-          half4_t{(_Float16)th[0], (_Float16)th[1], (_Float16)th[2], (_Float16)th[3]};
-      const half8_t thv = *(const half8_t*)(th_w + (t * 16 + ql) * 32 + 16 * (g - GTH > 0 ? 1 : 0));
-      half8_t q2 = qin2 ? qf[t][2] : half8_t{};
-      qf[t][2] = thl ? thv : q2;
+      th[t][0] = *(const half8_t*)(thx + (t * 16 + ql) * 32);
+      th[t][1] = *(const half8_t*)(thx + (t * 16 + ql) * 32 + 16);
     }
 
-    const char* kb = bufs + buf * BUFB;
-    const char* vb = kb + KC * 16;
-
-    // ---- scores S^T = K'.Q'^T + TW for all key rows
+    // ---- scores S^T = K.Q^T + TW + TH for all key rows (next row's K fragments in flight)
     float4_t sc[QT][S];
+    half8_t kf[2][KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) kf[0][s] = *(const half8_t*)(smem + s * 1024 + lane * 16);
 #pragma unroll
     for (int kh = 0; kh < S; ++kh) {
-      half8_t kf[KS];
+      if (kh + 1 < S) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) kf[s] = *(const half8_t*)(kb + (kh * S + ql) * KROW + (32 * s + 8 * g) * 2);
+        for (int s = 0; s < KS; ++s) kf[(kh + 1) & 1][s] = *(const half8_t*)(smem + (kh + 1) * ROWB + s * 1024 + lane * 16);
+      }
 #pragma unroll
       for (int t = 0; t < QT; ++t) {
-        float4_t a = tw[t];
+        const float h = (float)th[t][kh >> 3][kh & 7];
+        float4_t a = tw[t] + h;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[s], qf[t][s], a, 0, 0, 0);
+        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kh & 1][s], qf[t][s], a, 0, 0, 0);
         sc[t][kh] = a;
       }
-      __builtin_amdgcn_sched_barrier(0);   // keep the K' loads of row kh next to their MFMAs
+      __builtin_amdgcn_sched_barrier(0);   // no hoisting of later rows' C inputs (register pressure)
+    }
+    // next pass's operands stream in behind the softmax / PV
+    if (SAMQ_WIN_PREFETCH && pass + 1 < npass) {
+#pragma unroll
+      for (int t = 0; t < QT; ++t) {
+        load_q(row0 + 8 + t, qraw[t]);
+        load_rel(row0 + 8 + t, relh[t], relw[t]);
+      }
     }
 
     // ---- exact softmax over the window (exp2 domain)
     half8_t pb[QT][S / 2];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      float mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
-      mx = max3f(mx, sc[t][0][3], sc[t][1][0]);
-      mx = max3f(mx, sc[t][1][1], sc[t][1][2]);
-      mx = fmaxf(mx, sc[t][1][3]);
+      float m[S];
 #pragma unroll
-      for (int kh = 2; kh < S; ++kh) {
-        mx = max3f(mx, sc[t][kh][0], sc[t][kh][1]);
-        mx = max3f(mx, sc[t][kh][2], sc[t][kh][3]);
-      }
+      for (int kh = 0; kh < S; ++kh) m[kh] = max3f(sc[t][kh][0], sc[t][kh][1], fmaxf(sc[t][kh][2], sc[t][kh][3]));
+      float mx = max3f(m[0], m[1], m[2]);
+      float my = max3f(m[3], m[4], m[5]);
+      float mz = max3f(m[6], m[7], m[8]);
+      float mw = max3f(m[9], m[10], m[11]);
+      mx = max3f(mx, my, fmaxf(m[12], m[13]));
+      mx = max3f(mx, mz, mw);
       mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
 #pragma unroll
@@ -726,32 +717,27 @@ __global__ __launch_bounds__(64 * 7, 1) void win_attention_kernel(AttnParams p, 
         }
     }
 
-    // ---- O^T = V^T . P^T (two key rows per MFMA; V^T fragments of the next pair in flight),
-    // l = ones . P^T
-    float4_t o[QT][DT], lsum[QT];
-#pragma unroll
-    for (int t = 0; t < QT; ++t) {
-      lsum[t] = float4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int d = 0; d < DT; ++d) o[t][d] = float4_t{0.f, 0.f, 0.f, 0.f};
-    }
-    const uint32_t vaddr = lds_addr(vb + ((4 * g + trow) * D + tcol) * 2);
+    // ---- O^T = V^T . P^T (two key rows per MFMA), l = ones . P^T
+    float4_t o[QT][DT], lsum[QT];   // first written by the pr = 0 MFMAs (zero C operand)
+    const float4_t zero4 = {0.f, 0.f, 0.f, 0.f};
     half4_t vlo[2][DT], vhi[2][DT];
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      vlo[0][d] = ds_read_tr16(vaddr + d * 32);
-      vhi[0][d] = ds_read_tr16(vaddr + S * D * 2 + d * 32);
-    }
-#pragma unroll
-    for (int pr = 0; pr < S / 2; ++pr) {
-      const int cb = pr & 1;
-      if (pr + 1 < S / 2) {
-#pragma unroll
-        for (int d = 0; d < DT; ++d) {
-          vlo[cb ^ 1][d] = ds_read_tr16(vaddr + (2 * pr + 2) * S * D * 2 + d * 32);
-          vhi[cb ^ 1][d] = ds_read_tr16(vaddr + (2 * pr + 3) * S * D * 2 + d * 32);
-        }
-      }
+    // V^T fragments of key rows (2 pr, 2 pr + 1) for all d tiles (immediate offsets from two bases)
+    auto vread = [&](auto prc, half4_t (&lo)[DT], half4_t (&hi)[DT]) {
+      constexpr int PR = decltype(prc)::value;
+      constexpr int HB = PR >= 4 ? 32768 : 0;
+      const uint32_t base = vlane + HB;
+      static_for<DT>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        constexpr int VO = d < 4 ? V0 + (d >> 1) * 1024 + (d & 1) * 512 : 2 * 1024 + 512;
+        lo[d] = ds_read_tr16_off<(2 * PR) * ROWB + VO - HB>(base);
+        hi[d] = ds_read_tr16_off<(2 * PR + 1) * ROWB + VO - HB>(base);
+      });
+    };
+    vread(std::integral_constant<int, 0>{}, vlo[0], vhi[0]);
+    static_for<S / 2>([&](auto prc) {
+      constexpr int pr = decltype(prc)::value;
+      constexpr int cb = pr & 1;
+      if constexpr (pr + 1 < S / 2) vread(std::integral_constant<int, pr + 1>{}, vlo[cb ^ 1], vhi[cb ^ 1]);
       // this pair's fragments landed (the next pair's 2*DT reads may still be in flight)
       if constexpr (DT == 5) {
         if (pr + 1 < S / 2)
@@ -773,44 +759,36 @@ __global__ __launch_bounds__(64 * 7, 1) void win_attention_kernel(AttnParams p, 
         const half8_t va = {vlo[cb][d][0], vlo[cb][d][1], vlo[cb][d][2], vlo[cb][d][3],
                             vhi[cb][d][0], vhi[cb][d][1], vhi[cb][d][2], vhi[cb][d][3]};
 #pragma unroll
-        for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][pr], o[t][d], 0, 0, 0);
+        for (int t = 0; t < QT; ++t)
+          o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][pr], pr ? o[t][d] : zero4, 0, 0, 0);
       }
 #pragma unroll
-      for (int t = 0; t < QT; ++t) lsum[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pb[t][pr], lsum[t], 0, 0, 0);
-    }
+      for (int t = 0; t < QT; ++t)
+        lsum[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pb[t][pr], pr ? lsum[t] : zero4, 0, 0, 0);
+    });
 
     // ---- normalise + store (token-major [B, H, W, C])
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      const int qr = wave * QT + t;
-      if (qr >= S || ql >= S || cur.Y0 + qr >= p.H || cur.X0 + ql >= p.W) continue;
+      const int r = row0 + t;
+      if (r >= nrow || ql >= ncol) continue;
       const float inv = 1.0f / lsum[t][0];
-      _Float16* dst = p.out + (((int64_t)cur.b * p.H + (cur.Y0 + qr)) * p.W + (cur.X0 + ql)) * C + cur.head * D;
+      _Float16* dst = p.out + (((int64_t)b * p.H + (Y0 + r)) * p.W + (X0 + ql)) * C + head * D;
 #pragma unroll
       for (int d = 0; d < DT; ++d) {
         half4_t v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (_Float16)(o[t][d][r] * inv);
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)(o[t][d][e] * inv);
         *(half4_t*)(dst + d * 16 + 4 * g) = v;
       }
     }
-
-    if (!has_next) break;
-    ++it;
-    item = nitem;
-    cur = nxt;
-    buf ^= 1;
   }
 }
 
 template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  int grid = cus < items ? cus : items;
-  grid = (grid + 7) & ~7;   // multiple of 8 (XCD-aware item numbering); surplus workgroups exit
-  hipLaunchKernelGGL((win_attention_kernel<D>), dim3(grid), dim3(64 * 7), 0, stream, p, items);
+  hipLaunchKernelGGL((win_attention_kernel<D>), dim3(items), dim3(256), 0, stream, p, items);
   SAMQ_LAUNCH_CHECK("win_attention launch");
   return SAMQ_OK;
 }
@@ -836,7 +814,7 @@ static int launch_attn(const AttnParams& p, int units, hipStream_t stream) {
 template <bool PRE>
 static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t stream) {
   const int S = p.S;
-  if (!PRE && S == 14)   // SAM's window size: persistent double-buffered kernel
+  if (!PRE && S == 14)   // SAM's window size: two-workgroups-per-CU window kernel
     return hd == 80 ? launch_win<80>(p, units, stream) : launch_win<64>(p, units, stream);
   if (S <= 16) {  // whole window / small grid resident in LDS; one query tile per grid row
     if (S == 14)
