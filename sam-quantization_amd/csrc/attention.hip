@@ -641,7 +641,7 @@ __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int
       for (int s = 0; s < KS; ++s) {
         half8_t v = qraw[t][s];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)((float)v[j] * qscale);
+        for (int j = 0; j < 8; ++j) v[j] = (_Float16)__builtin_fmaf((float)v[j], qscale, 0.0f);   // v_fma_mix
         qf[t][s] = v;
       }
       float4_t a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
@@ -697,15 +697,18 @@ __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int
     half8_t pb[QT][S / 2];
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
-      float m[S];
+      // two independent max3 chains (no canonicalising v_max of a lone fmaxf)
+      float mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
+      float my = max3f(sc[t][1][0], sc[t][1][1], sc[t][1][2]);
+      mx = max3f(mx, sc[t][0][3], sc[t][1][3]);
 #pragma unroll
-      for (int kh = 0; kh < S; ++kh) m[kh] = max3f(sc[t][kh][0], sc[t][kh][1], fmaxf(sc[t][kh][2], sc[t][kh][3]));
-      float mx = max3f(m[0], m[1], m[2]);
-      float my = max3f(m[3], m[4], m[5]);
-      float mz = max3f(m[6], m[7], m[8]);
-      float mw = max3f(m[9], m[10], m[11]);
-      mx = max3f(mx, my, fmaxf(m[12], m[13]));
-      mx = max3f(mx, mz, mw);
+      for (int kh = 2; kh < S; kh += 2) {
+        mx = max3f(mx, sc[t][kh][0], sc[t][kh][1]);
+        my = max3f(my, sc[t][kh + 1][0], sc[t][kh + 1][1]);
+        mx = max3f(mx, sc[t][kh][2], sc[t][kh][3]);
+        my = max3f(my, sc[t][kh + 1][2], sc[t][kh + 1][3]);
+      }
+      mx = fmaxf(mx, my);
       mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
 #pragma unroll
@@ -772,7 +775,7 @@ __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int
     for (int t = 0; t < QT; ++t) {
       const int r = row0 + t;
       if (r >= nrow || ql >= ncol) continue;
-      const float inv = 1.0f / lsum[t][0];
+      const float inv = __builtin_amdgcn_rcpf(lsum[t][0]);
       _Float16* dst = p.out + (((int64_t)b * p.H + (Y0 + r)) * p.W + (X0 + ql)) * C + head * D;
 #pragma unroll
       for (int d = 0; d < DT; ++d) {

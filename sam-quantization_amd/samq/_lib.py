@@ -10,9 +10,11 @@ import ctypes
 import os
 from pathlib import Path
 
-# SAMQ_LIB=tuning selects the tuning build (make tuning: adds timing-only tile configs); tools only
-LIB_PATH = Path(__file__).resolve().parent / (
-    "libsamq_hip_tuning.so" if os.environ.get("SAMQ_LIB") == "tuning" else "libsamq_hip.so")
+# SAMQ_LIB=tuning selects the tuning build (make tuning: adds timing-only tile configs) and
+# SAMQ_LIB=<path>.so a kernel-variant build for A/B runs; tools only
+_sel = os.environ.get("SAMQ_LIB", "")
+LIB_PATH = (Path(_sel) if _sel.endswith(".so") else Path(__file__).resolve().parent / (
+    "libsamq_hip_tuning.so" if _sel == "tuning" else "libsamq_hip.so"))
 
 SAMQ_OK = 0
 SAMQ_ERR_INVALID = -1
