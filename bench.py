@@ -134,24 +134,45 @@ def source_hash() -> str:
     return h.hexdigest()[:12]
 
 
-def in_step_from_profile(mode, imgs_per_launch, lanes, flops_launch, peak):
-    """GEMM roofline of the timed replays (concurrent lanes included) from the committed rocprof
-    kernel stats: average algorithmic FLOPs per launch / average GEMM dispatch duration."""
-    name = f"instep_{mode}_b{imgs_per_launch}_l{lanes}_{source_hash()}.csv"
-    f = REPO / "profiles" / name
-    if not f.exists() or not flops_launch:
+def _roctx():
+    try:
+        import ctypes
+        return ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+    except OSError:
         return None
-    import csv
+
+
+def is_proj_gemm(mode, name):
+    """Is a dispatch one of the mode's projection GEMMs (qkv / proj / lin1 / lin2 [+ the W8A8 neck
+    1x1, an int8 GEMM of the same kernel)?  i8_gemm_kernel<BM, BN, WM, WN, EPI, W4, ., AG>: W4
+    selects the int4-weight form, AG = 0 the plain row-major A operand (not the implicit convs)."""
+    if mode == "w4a16":
+        return "w4a16_gemm" in name
+    if "i8_gemm_kernel<" not in name:
+        return False
+    args = [a.strip() for a in name.split("i8_gemm_kernel<", 1)[1].split(">", 1)[0].split(",")]
+    return args[5] == ("1" if mode == "w4a8" else "0") and args[7] == "0"
+
+
+def in_step_from_profile(mode, imgs_per_launch, lanes, flops_step, peak):
+    """GEMM roofline of the timed replays (concurrent lanes included) from the committed rocprof
+    kernel trace, restricted to bench's roctx-marked timed window: GEMM FLOPs of the window /
+    summed GEMM dispatch time (tools/instep_profile.sh writes the JSON)."""
+    name = f"instep_{mode}_b{imgs_per_launch}_l{lanes}_{source_hash()}.json"
+    f = REPO / "profiles" / name
+    if not f.exists() or not flops_step:
+        return None
+    d = json.loads(f.read_text())
     tot_ns = n = 0
-    for r in csv.DictReader(open(f)):
-        if "w4a16_gemm" in r["Name"]:
-            tot_ns += float(r["TotalDurationNs"])
-            n += int(r["Calls"])
+    for k, v in d["kernels"].items():
+        if is_proj_gemm(mode, k):
+            tot_ns += v["total_ns"]
+            n += v["calls"]
     if not n:
         return None
-    ach = flops_launch / (tot_ns / n * 1e-9) / 1e12
+    ach = flops_step * d["steps"] / (tot_ns * 1e-9) / 1e12
     return dict(achieved=round(ach, 1), frac=round(ach / peak, 4), avg_launch_us=round(tot_ns / n / 1e3, 2),
-                dispatches=n, source=f"profiles/{name}")
+                dispatches=n, steps=d["steps"], window_ms=d["window_ms"], source=f"profiles/{name}")
 
 
 def _time_launches(launches, reps=3):
@@ -212,6 +233,18 @@ def w8a8_roofline(eng, batch: int):
                 frac=round(achieved / PEAK_INT8_TOPS, 4), traffic=None,
                 kernel="i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)", launches_timed=n,
                 avg_launch_us=round(t / n * 1e6, 2))
+
+
+def gemm_flops_per_step(mode, eng, images):
+    """Algorithmic FLOPs of the projection GEMMs (is_proj_gemm) of one step over ``images``."""
+    tok = images * 4096
+    if mode == "w8a8":
+        c = eng.embed_dim
+        tok = images * (eng.enc.img_size // eng.patch) ** 2
+        fl = sum(2.0 * tok * bl[k]["k"] * bl[k]["n"] for bl in eng.blocks for k in ("qkv", "proj", "lin1", "lin2"))
+        return fl + 2.0 * tok * c * 256                    # neck 1x1 (same kernel form)
+    return sum(2.0 * tok * lin.infeatures * lin.outfeatures
+               for p in eng.plans for lin in (p.qkv, p.proj, p.lin1, p.lin2))
 
 
 def cpu_baseline(model_name: str, mode: str = "w4a16"):
@@ -438,10 +471,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    rtx = _roctx()   # marks the timed window for tools/instep_profile.sh (no-op unprofiled)
+    if rtx:
+        rtx.roctxRangePushA(b"samq_timed_steps")
     t_start = time.perf_counter()
     for _ in range(args.steps):
         run()
     torch.cuda.synchronize()
+    if rtx:
+        rtx.roctxRangePop()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
@@ -469,17 +507,16 @@ def main():
         traffic, src = pmc_traffic("w4a16_gemm", profile) if profile else (None, None)
         kernel = "w4a16_gemm_pp2 (qkv, lin1) + w4a16_gemm_v3 (proj, lin2): all 4 ViT-H projection shapes"
         alg_b = round(sum(alg) / len(alg))
-        flops_launch = sum(2.0 * trows * lin.infeatures * lin.outfeatures
-                           for lin in (eng.plans[0].qkv, eng.plans[0].proj, eng.plans[0].lin1, eng.plans[0].lin2)) / 4
     else:
-        traffic, src, alg_b, flops_launch = None, None, None, None
+        traffic, src, alg_b = None, None, None
         kernel = ("i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)" if mode == "w4a8"
-                  else "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)")
+                  else "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes + neck 1x1)")
+    flops_step = gemm_flops_per_step(mode, eng, rows)
     live = dict(achieved=iso["achieved"], frac=iso["frac"], avg_launch_us=iso["avg_launch_us"],
                 launches_timed=iso["launches_timed"],
                 method="HIP events on the launch stream around every GEMM launch of one forward at the lane's "
                        "size, back to back with no concurrent lane (3 reps)")
-    ins = in_step_from_profile(mode, per_launch_imgs, args.lanes, flops_launch, peak)
+    ins = in_step_from_profile(mode, per_launch_imgs, args.lanes, flops_step, peak)
     head = ins if ins else live
     roof = dict(bound="mfma", achieved=head["achieved"], peak=peak, unit="TFLOP/s", frac=head["frac"],
                 traffic=traffic, traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,

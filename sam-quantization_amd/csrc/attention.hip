@@ -324,19 +324,33 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
           for (int r = 0; r < 4; ++r)
             if (kt * 16 + 4 * g + r >= S) sc[t][kt][r] = -INFINITY;
       }
-      float mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
-      mx = max3f(mx, sc[t][0][3], mx);
+      float mx;
+      if constexpr (KT == 1) {
+        mx = max3f(sc[t][0][0], sc[t][0][1], fmaxf(sc[t][0][2], sc[t][0][3]));
+      } else {   // two max3 chains (no canonicalising v_max of a lone fmaxf)
+        mx = max3f(sc[t][0][0], sc[t][0][1], sc[t][0][2]);
+        float my = max3f(sc[t][1][0], sc[t][1][1], sc[t][1][2]);
+        mx = max3f(mx, sc[t][0][3], sc[t][1][3]);
 #pragma unroll
-      for (int kt = 1; kt < KT; ++kt) {
-        mx = max3f(mx, sc[t][kt][0], sc[t][kt][1]);
-        mx = max3f(mx, sc[t][kt][2], sc[t][kt][3]);
+        for (int kt = 2; kt < KT; kt += 2) {
+          mx = max3f(mx, sc[t][kt][0], sc[t][kt][1]);
+          my = max3f(my, sc[t][kt + 1][0], sc[t][kt + 1][1]);
+          mx = max3f(mx, sc[t][kt][2], sc[t][kt][3]);
+          my = max3f(my, sc[t][kt + 1][2], sc[t][kt + 1][3]);
+        }
+        mx = fmaxf(mx, my);
       }
       mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
-      mx = max3f(mx, __shfl_xor(mx, 16, 64), mx);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       const float th = th_w[(t * TH_ROWS + kh) * 16 + ql];
-      const float mnew = fmaxf(m[t], mx + th);
-      alpha[t] = __builtin_amdgcn_exp2f(m[t] - mnew);
-      any_rescale |= mnew != m[t];
+      // lazy rescale: the exp2 offset m only moves when the row max exceeds it by > 8 (P <= 2^8,
+      // far inside fp16; O and l carry the same offset, so O / l is unchanged) -- most key rows
+      // then skip the O rescale, whose packed multiplies beside the MFMAs bound this loop
+      const float mrow = mx + th;
+      const bool up = mrow > m[t] + 8.0f;
+      const float mnew = up ? mrow : m[t];
+      alpha[t] = up ? __builtin_amdgcn_exp2f(m[t] - mnew) : 1.0f;
+      any_rescale |= up;
       m[t] = mnew;
       const float corr = mnew - th;
       float rs = 0.f;
