@@ -1290,24 +1290,17 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
 // The ping-pong v6 (cfg 57: 256x256 tiles, 4-slot ring, lookahead 3) is 5-7 % faster on the wide
 // projections (qkv N=3840, lin1 N=5120 at M=16384: 1090 / 970 TF/s vs 1016 / 925); with N=1280 its
 // 320 tiles leave a 25 % second round on 256 CUs, where v3's 2-workgroup/CU 128x256 stays ahead.
-// 128x320 tiles (cfg 29) when they make exactly one round on the chip: the N=1280 projections
-// of one 2-image lane (M = 8192: 64 x 4 = 256 tiles) run proj 38 vs 42 us and lin2 105 vs 124 us
-// against cfg 22 (profiles/r1_v12_gemm_scan_m8192.log); at M = 16384 cfg 22 stays ahead.
-static int num_cus() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, c = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-    cus = c > 0 ? c : 256;
-  }
-  return cus;
-}
-
+// 128x320 tiles (cfg 29) make exactly one round on the chip for the N=1280 projections of one
+// 2-image lane (M = 8192: isolated proj 38 vs 42 us, lin2 105 vs 124 us against cfg 22,
+// profiles/r1_v12_gemm_scan_m8192.log) but are the slowest per CU in steady state; see pick_cfg.
 static int pick_cfg(int M, int N, bool grouped) {
-  if (!grouped && N % 320 == 0 && N < 2048 && (int64_t)((M + 127) / 128) * (N / 320) == num_cus()) return 29;
   // v6 from two images up: at M = 4096 (one image) lin1 runs 63.5 us on cfg 22 vs 77.9 on v6 and
-  // qkv is a tie (profiles/r1_v20_gemm_scan_m4096.log)
-  if (!grouped && N % 256 == 0 && N >= 2048 && M >= 8192) return 57;
+  // qkv is a tie (profiles/r1_v20_gemm_scan_m4096.log).  The N = 1280 projections (proj, lin2)
+  // take v6 on 16x16x32 MFMA (cfg 64): in steady state (M = 65536, no tile-round tail) lin2 runs
+  // 1161 TF/s there vs 969 on the one-round 128x320 tiles (cfg 29) that win an isolated M = 8192
+  // launch, and inside the 2-lane graph -- where the other lane fills any tail -- the step drops
+  // 25.66 -> 24.35 ms with bit-identical output (profiles/r2_cfg_ab.log)
+  if (!grouped && N % 256 == 0 && M >= 8192) return N >= 2048 ? 57 : 64;
   if (N % 256 == 0 && M >= 1024) return 22;
   if (N % 128 == 0 && M >= 512) return 23;
   if (N % 64 == 0) return 26;

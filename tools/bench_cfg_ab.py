@@ -14,7 +14,10 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"pick": {}, "lin1=22": {"lin1": 22}, "qkv=56": {"qkv": 56}, "lin1=22,qkv=22": {"lin1": 22, "qkv": 22}}
+VARIANTS = {"p64,l2=64": {"proj": 64, "lin2": 64}, "all64": {"proj": 64, "lin2": 64, "qkv": 64, "lin1": 64},
+            "p64,l2=64,qkv=64": {"proj": 64, "lin2": 64, "qkv": 64},
+            "p64,l2=64,lin1=64": {"proj": 64, "lin2": 64, "lin1": 64},
+            "p64,l2=64,lin1=22": {"proj": 64, "lin2": 64, "lin1": 22}, "pick": {}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 eng = enc.engine()
