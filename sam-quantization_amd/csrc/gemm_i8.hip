@@ -381,11 +381,14 @@ static int i8_cfg_bn(int cfg) {
 }
 
 static int i8_pick_cfg(int M, int N, int bfmt) {
-  // W4 at ViT-H sizes (tools/bench_i8.py, M = 16384 / 32768, profiles/r1_v11_i8_scan.log): the
-  // wide projections (qkv, lin1: N >= 2560) run best on 256x256 tiles, the N=1280 ones (proj,
-  // lin2) on 128x128 tiles (1280 tiles per 16384 rows: 5 even rounds of 256 CUs, not 1.25).
+  // W4 at ViT-H sizes: 256x256 tiles for all four projections.  In steady state (tools/bench_i8.py
+  // --m 65536: no tile-round tail) they are the fastest per CU on every shape (lin2 1717 TOPS vs
+  // 1602 on 128x128, proj 857 vs 833), and inside the 2-lane W4A8 graph -- the other lane fills
+  // tails -- proj / lin2 on them take the step 40.06 -> 38.29 ms, bit-identical
+  // (tools/bench_cfg_ab_w4a8.py, profiles/r2_cfg_ab_w4a8.log); the round-1 pick of 128x128 for
+  // N = 1280 came from isolated M = 16384 launches (profiles/r1_v11_i8_scan.log).
   if (bfmt == BF_W4 && M >= 8192) {
-    if (N % 256 == 0 && N >= 2560) return 81;
+    if (N % 256 == 0) return 81;
     if (N % 128 == 0) return 83;
   }
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);

@@ -352,11 +352,11 @@ def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: to
 
 
 def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_scale=1.0, out_scale=0.0,
-              out=None, groupsize=-1):
-    """GPTQ int4 weights (repacked layout 3) x int8 activation codes."""
+              out=None, groupsize=-1, cfg=0):
+    """GPTQ int4 weights (repacked layout 3) x int8 activation codes (cfg 0 = library pick)."""
     if groupsize not in (-1, a.shape[-1]):
         raise NotImplementedError("w4a8_gemm: only groupsize -1 (per-channel) is supported with int8 activations")
-    return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out)
+    return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out, cfg=cfg)
 
 
 def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,

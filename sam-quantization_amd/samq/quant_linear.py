@@ -112,7 +112,7 @@ class QuantLinear(nn.Module):
         """int8 input codes (scale ``a_scale``) x int4 weights on the int8 MFMA."""
         w = self.prepare_w4a8()
         return ops.w4a8_gemm(codes, w["packed"], w["scale"], self.qzeros, self.outfeatures, w["bias"], epilogue,
-                             a_scale, out_scale, out=out)
+                             a_scale, out_scale, out=out, cfg=getattr(self, "i8_cfg", 0))
 
     def forward_epilogue(self, x: torch.Tensor, epilogue: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         assert x.shape[-1] == self.qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
