@@ -427,7 +427,9 @@ def main():
             ap.error("--mode w8a8 runs one kernel chain (W8A8Engine has no lanes)")
         args.lanes = 1
     elif args.lanes <= 0:
-        args.lanes = 2 if batch % 2 == 0 else 1
+        # W4A16: two images per lane (M = 8192 per GEMM launch, the size the tile picks and the
+        # quoted roofline are tuned on; B=8 on 4 lanes 48.30 vs 49.02 ms on 2, tools/bench_lanes.py)
+        args.lanes = (batch // 2 if mode == "w4a16" else 2) if batch % 2 == 0 else 1
     if batch % args.lanes:
         ap.error(f"--lanes {args.lanes} does not divide the per-GPU batch {batch}")
 

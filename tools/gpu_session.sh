@@ -34,6 +34,7 @@ for step in "$@"; do
     benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     instep)  run instep 500 bash tools/instep_profile.sh w4a16 ;;
     instep48) run instep48 500 bash tools/instep_profile.sh w4a8 ;;
+    instepb8) run instepb8 500 bash tools/instep_profile.sh w4a16 --batch 8 ;;
     instep88) run instep88 500 bash tools/instep_profile.sh w8a8 ;;
     prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -3,16 +3,17 @@
 # live roofline passes); the dispatches inside bench's roctx "samq_timed_steps" range ->
 # gpurun_out/instep_<mode>_b<imgs/launch>_l<lanes>_<source hash>.json (copy into profiles/: bench.py
 # reads its in-step GEMM roofline from it), plus the whole-run --stats summary next to it.
-# usage: tools/instep_profile.sh [w4a16|w4a8|w8a8]
+# usage: tools/instep_profile.sh [w4a16|w4a8|w8a8] [extra bench.py args, e.g. --batch 8]
 set -eu
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mode=${1:-w4a16}
+shift || true
 steps=10
 d=gpurun_out/instep_$mode
 rm -rf "$d"
 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats -d "$d" -o run --output-format csv -- \
-  python3 bench.py --mode "$mode" --steps $steps --warmup 3 --no-cpu-baseline --no-isolated > "$d.log" 2>&1
+  python3 bench.py --mode "$mode" --steps $steps --warmup 3 --no-cpu-baseline --no-isolated "$@" > "$d.log" 2>&1
 name=$(python3 - "$mode" <<'PY'
 import json, sys
 sys.path.insert(0, ".")
