@@ -296,11 +296,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
       for (int kt = 0; kt < KT; ++kt) {
         const char* krow = kb + (kt * 16 + ql) * (D * 2);
         half8_t kf[KS];
+        // unconditional: lanes past D in the last k-step read the next key's bytes (finite K/V
+        // data of the LDS image) against zero Q dims -- no v_mov zero-fill per fragment
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          kf[s] = half8_t{};
-          if (s < 2 || kin3) kf[s] = *(const half8_t*)(krow + (32 * s + 8 * g) * 2);
-        }
+        for (int s = 0; s < KS; ++s) kf[s] = *(const half8_t*)(krow + (32 * s + 8 * g) * 2);
 #pragma unroll
         for (int t = 0; t < QT; ++t) {
           float4_t a = tw[t][kt];
@@ -389,23 +388,23 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   };
   auto pv = [&](const char* vb, PB& pb, half4_t (&pb16)[QT]) {
     // ---- O^T += V^T . P^T  (V^T fragments by hardware-transposed LDS reads of row-major V)
-#pragma unroll
-    for (int d = 0; d < DT; ++d) {
+    // one base address per key row, the (d, s) offsets as the instruction's immediate
+    const uint32_t vbase = lds_addr(vb + ((4 * g + trow) * D + tcol) * 2);
+    static_for<DT>([&](auto dc_) {
+      constexpr int d = decltype(dc_)::value;
       if constexpr (SP == 16) {
-        const char* a0 = vb + ((4 * g + trow) * D + d * 16 + tcol) * 2;
-        const half4_t va = __builtin_bit_cast(
-            half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0)));
+        half4_t va = ds_read_tr16_off<(d * 16) * 2>(vbase);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(va));
 #pragma unroll
         for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x16f16(va, pb16[t], o[t][d], 0, 0, 0);
       } else {
         constexpr int NS = SP / 32;
         half4_t lo[NS], hi[NS];
-        const uint32_t vaddr = lds_addr(vb + ((4 * g + trow) * D + d * 16 + tcol) * 2);
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          lo[s] = ds_read_tr16(vaddr + (32 * s) * D * 2);
-          hi[s] = ds_read_tr16(vaddr + (32 * s + 16) * D * 2);
-        }
+        static_for<NS>([&](auto sc_) {
+          constexpr int s_ = decltype(sc_)::value;
+          lo[s_] = ds_read_tr16_off<((32 * s_) * D + d * 16) * 2>(vbase);
+          hi[s_] = ds_read_tr16_off<((32 * s_ + 16) * D + d * 16) * 2>(vbase);
+        });
         if constexpr (NS == 2) {
           asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[0]), "+v"(hi[0]), "+v"(lo[1]), "+v"(hi[1]));
         } else {
@@ -419,7 +418,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
           for (int t = 0; t < QT; ++t) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][s], o[t][d], 0, 0, 0);
         }
       }
-    }
+    });
     if constexpr (MSUM) {
       constexpr int NS = SP / 32;
 #pragma unroll
