@@ -10,20 +10,21 @@ export TMPDIR=/tmp
 mode=${1:-w4a16}
 shift || true
 steps=10
-d=gpurun_out/instep_$mode
+tag=$(echo "$*" | tr -c 'a-zA-Z0-9' '_')
+d=gpurun_out/instep_$mode$tag
 rm -rf "$d"
 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats -d "$d" -o run --output-format csv -- \
   python3 bench.py --mode "$mode" --steps $steps --warmup 3 --no-cpu-baseline --no-isolated "$@" > "$d.log" 2>&1
-name=$(python3 - "$mode" <<'PY'
+name=$(python3 - "$mode" "$d.log" <<'PY'
 import json, sys
 sys.path.insert(0, ".")
 import bench
-line = [l for l in open(f"gpurun_out/instep_{sys.argv[1]}.log") if l.startswith("{")][-1]
+line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
 c = d["config"]
 print(f"instep_{sys.argv[1]}_b{c['per_gpu_batch'] // c['lanes']}_l{c['lanes']}_{bench.source_hash()}")
 PY
 )
-python3 tools/instep_window.py "$d" $steps "gpurun_out/$name.json"
+python3 tools/instep_window.py "$d" $steps "gpurun_out/$name.json" "$mode"
 cp "$d/run_kernel_stats.csv" "gpurun_out/${name}_wholerun_stats.csv"
 echo "in-step profile: gpurun_out/$name.json (copy into profiles/)"
