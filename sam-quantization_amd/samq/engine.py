@@ -45,6 +45,7 @@ class EncoderEngine:
         self.device = enc.pos_embed.device if enc.pos_embed is not None else next(enc.parameters()).device
         self.C = enc.embed_dim
         self.grid = enc.img_size // enc.patch_size
+        self.ln_rpw = 0   # LayerNorm rows per wave (0 = library default; in-graph A/B knob)
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
@@ -194,11 +195,11 @@ class EncoderEngine:
         if self.w4a8:
             return self.block_w4a8(p, bufs)
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
-        ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn)
+        ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw)
         p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
         p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
-        ops.layernorm(x, p.ln2_w, p.ln2_b, p.ln2_eps, out=xn)
+        ops.layernorm(x, p.ln2_w, p.ln2_b, p.ln2_eps, out=xn, rows_per_wave=self.ln_rpw)
         p.lin1.forward_epilogue(xn, ops.EPI_BIAS_GELU, out=hid)
         p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
 

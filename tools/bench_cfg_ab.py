@@ -14,10 +14,7 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"p64,l2=64": {"proj": 64, "lin2": 64}, "all64": {"proj": 64, "lin2": 64, "qkv": 64, "lin1": 64},
-            "p64,l2=64,qkv=64": {"proj": 64, "lin2": 64, "qkv": 64},
-            "p64,l2=64,lin1=64": {"proj": 64, "lin2": 64, "lin1": 64},
-            "p64,l2=64,lin1=22": {"proj": 64, "lin2": 64, "lin1": 22}, "pick": {}}
+VARIANTS = {"pick": {}, "ln_rpw=1": {"ln_rpw": 1}, "ln_rpw=4": {"ln_rpw": 4}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 eng = enc.engine()
@@ -25,6 +22,7 @@ g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((4, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
+    eng.ln_rpw = cfg.get("ln_rpw", 0)
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).gemm_cfg = cfg.get(lay, 0)
