@@ -127,6 +127,25 @@ def test_w4a16_gemm_auto_pick_wide(cuda, groupsize):
         _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, 0, rng)
 
 
+@pytest.mark.parametrize("n", [1280, 2560])
+def test_w4a16_gemm_auto_pick_lane(cuda, n):
+    """The automatic tile choice at one 2-image lane (M = 8192): the 16x16x32 ping-pong (cfg 64)
+    for the N = 1280 projections, the 32x32x16 one (cfg 57) for wide N -- against the oracle, and
+    bit-identical to the explicit config."""
+    from samq import ops
+    m, k = 8192, 1280
+    qw, qz, sc, bias = _packed_layer(k, n, -1, seed=91 + n)
+    rng = np.random.Generator(np.random.PCG64(92))
+    a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+    y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
+    packed = ops.w4_repack(_dev(qw, cuda))
+    for epi in ("bias", "resadd"):
+        _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, -1, epi, 0, rng)
+    args = (_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, -1)
+    auto = ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=0)
+    assert torch.equal(auto, ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=64 if n < 2048 else 57))
+
+
 @pytest.mark.parametrize("tag", ["gm1", "g128"])
 def test_matmul4_functional_vs_reference_golden(cuda, golden_dir, tag):
     """``triton_matmul4`` drop-in on the reference's own fixture: within fp16 rounding of the
