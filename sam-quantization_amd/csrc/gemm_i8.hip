@@ -73,6 +73,112 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
   }
 }
 
+// y = float(acc) * (a_scale * wscale[n]) + bias[n] (-> GELU / residual / int8 quantiser), staged
+// through LDS in 32-row slices per wave (ep = this wave's 32 x WN f32 slice) so the global traffic
+// is row-contiguous 16-byte vectors.  Shared by the v3-style and the ping-pong int8 kernels.
+template <int TM, int TN, int WN, int EPI>
+__device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], const int (&col)[TN],
+                                            const float* __restrict__ wscale, const float* __restrict__ bias,
+                                            const I8Epi& ep_args, float* ep, void* __restrict__ Cout, int64_t ldc,
+                                            int M, int row_base, int col_base, int lane) {
+  const int hsel = lane >> 5;
+  float csc[TN], cb[TN];
+#pragma unroll
+  for (int t = 0; t < TN; ++t) {
+    csc[t] = ep_args.a_scale * wscale[col[t]];
+    cb[t] = bias ? bias[col[t]] : 0.0f;
+  }
+  constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
+  const float inv_out = ep_args.out_scale > 0.f ? 1.0f / ep_args.out_scale : 0.f;   // q8_exact (common.h)
+  const float inv_mid = ep_args.mid_scale > 0.f ? 1.0f / ep_args.mid_scale : 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        float v = (float)acc[i][t][r] * csc[t] + cb[t];
+        if (GELU) v = gelu_fast(v);
+        ep[rl * WN + t * 32 + (lane & 31)] = v;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+      constexpr int C4 = WN / 4;
+#pragma unroll
+      for (int j = 0; j < 32 * C4 / 64; ++j) {
+        const int idx = j * 64 + lane;
+        const int rl = idx / C4, c4 = idx % C4;
+        const int row = row_base + i * 32 + rl;
+        const float4_t v = ((const float4_t*)ep)[idx];
+        if (row < M) {
+          float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
+          if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+        }
+      }
+    } else if (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) {
+      constexpr int C8 = WN / 8;
+#pragma unroll
+      for (int j = 0; j < (32 * C8 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < 32 * C8) {
+          const int rl = idx / C8, c8 = idx % C8;
+          const int row = row_base + i * 32 + rl;
+          const float4_t v0 = ((const float4_t*)ep)[2 * idx];
+          const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+          if (row < M) {
+            const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                               (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+            *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
+          }
+        }
+      }
+    } else {   // int8 codes, 16 columns per lane-store
+      constexpr int C16 = WN / 16;
+#pragma unroll
+      for (int j = 0; j < (32 * C16 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < 32 * C16) {
+          const int rl = idx / C16, c16 = idx % C16;
+          const int row = row_base + i * 32 + rl;
+          if (row < M) {
+            float v[16];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float4_t f = ((const float4_t*)ep)[4 * idx + e];
+              v[4 * e] = f[0]; v[4 * e + 1] = f[1]; v[4 * e + 2] = f[2]; v[4 * e + 3] = f[3];
+            }
+            u32x4 res;
+            if (EPI == SAMQ_EPI_Q8_RES)
+              res = *(const u32x4*)(ep_args.R + (int64_t)(ep_args.rmod > 0 ? row % ep_args.rmod : row) * ep_args.ldr +
+                                    col_base + 16 * c16);
+            u32x4 o;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+              uint32_t word = 0;
+#pragma unroll
+              for (int b = 0; b < 4; ++b) {
+                float x = v[4 * w + b];
+                if (EPI == SAMQ_EPI_Q8_RES) {
+                  if (ep_args.mid_scale > 0.f) x = q8_exact(x, ep_args.mid_scale, inv_mid) * ep_args.mid_scale;
+                  const float rv = (float)(int8_t)((res[w] >> (8 * b)) & 0xFFu) * ep_args.res_scale;
+                  x = rv + x;
+                }
+                const int qv = (int)q8_exact(x, ep_args.out_scale, inv_out);
+                word |= ((uint32_t)qv & 0xFFu) << (8 * b);
+              }
+              o[w] = word;
+            }
+            *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+}
+
 // ------------------------------------------------------------------ GEMM
 template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
@@ -245,107 +351,210 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   }
 
   // ---- epilogue (LDS-staged per 32-row slice; see gemm_w4a16.hip v3)
-  float csc[TN], cb[TN];
+  static_assert(NW * 32 * WN * 4 <= STAGES * STAGE, "epilogue staging does not fit the LDS ring");
+  __syncthreads();
+  i8_epilogue<TM, TN, WN, EPI>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * 32 * WN * 4), Cout, ldc, M,
+                               m0 + wm * WM, n0 + wn * WN, lane);
+}
+
+// ------------------------------------------------------------------ W4A8 ping-pong GEMM
+// The W4A16 v6 ping-pong structure (gemm_w4a16.hip w4a16_gemm_pp2) on the int8 MFMA: 256x256
+// tiles, 8 waves (2 x 4, 128x64 each) in two groups one s_barrier apart, so the two waves of a SIMD
+// alternate -- one issues its MFMA burst (s_setprio 1) while the other reads its A fragments and
+// its B piece from LDS and unpacks int4 -> int8; the LDS-DMA pieces of K tile kt+LA are issued
+// behind the MFMA bursts of tile kt.  K tile = 128 int8 (128-byte A rows, one 2-KiB layout-3 block
+// per 32 columns); phase p of a K tile = k32 steps 2p, 2p+1 = B piece p, so each phase reads its own
+// A fragments and unpacks its own piece.  WAR / RAW: as w4a16_gemm_pp2 (the slot restaged during
+// tile kt held tile kt+LA-STAGES <= kt-1, whose last reads were consumed before the barrier that
+// opens the MFMA half of tile kt's phase 0 for either group; the retire wait for tile kt+1 sits in
+// the load half of the last phase, before the barrier after which the first group reads it).
+__host__ __device__ constexpr int i8_pre(int p, int npw, int nph) {   // pieces issued before phase p
+  return (npw * p) / nph;
+}
+template <int N>
+__device__ __forceinline__ void i8_vm_wait_le(int n) {   // s_waitcnt vmcnt(n) for a uniform n <= N
+  if constexpr (N > 0) {
+    if (n >= N) { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); return; }
+    i8_vm_wait_le<N - 1>(n);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// VAR (tuning build only, timing experiments that compute wrong results): 1 no zero-point
+// subtraction in the unpack, 2 no MFMA, 4 no restaging
+template <int EPI, int STAGES, int LA, int VAR = 0>
+__global__ __launch_bounds__(512, 1)
+void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
+                 const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
+                 const float* __restrict__ bias, void* __restrict__ Cout, int64_t ldc, int M, int N, int K,
+                 I8Epi ep_args) {
+  constexpr int NW = 8, WAVES_N = 4, TM = 4, TN = 2;
+  constexpr int WM = TM * 32, WN = TN * 32;
+  constexpr int BM = 2 * WM, BN = WAVES_N * WN;
+  constexpr int BK = 128, ROWB = BK;
+  constexpr int A_BYTES = BM * ROWB;
+  constexpr int PPB = 2;                       // W4 layout 3: two 1-KiB pieces per (32 columns, 128 k)
+  constexpr int NA = BM / 8, NB = (BN / 32) * PPB, NT = NA + NB;
+  constexpr int NPW = (NT + NW - 1) / NW;
+  constexpr int STAGE = A_BYTES + NB * 1024;
+  constexpr int NPH = 2;
+  constexpr int PRE_LAST = i8_pre(NPH - 1, NPW, NPH);
+  constexpr int EP_BYTES = 32 * WN * 4;
+  constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
+  static_assert(LA >= 2 && LA < STAGES, "ring");
+  static_assert((LA - 2) * NPW + PRE_LAST <= 63 && (LA - 1) * NPW <= 63, "vmcnt");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+  const int grp = wave >> 2;
+  const int tiles_n = N / BN;
+  const int tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = K / BK;
+
+  const char* src[NPW];
+  int dst[NPW];
+  int step[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    int j = wave * NPW + i;
+    j = j < NT ? j : NT - 1;
+    if (j < NA) {
+      const int row = j * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((row >> 1) & 7);
+      int gr = m0 + row;
+      gr = gr < M ? gr : M - 1;
+      src[i] = (const char*)(A + (int64_t)gr * lda + c * 16);
+      dst[i] = j * 1024;
+      step[i] = BK;
+    } else {
+      const int jb = j - NA;
+      const int nt = n0 / 32 + jb / PPB;
+      src[i] = Wp + (((int64_t)nt * kt_count) * PPB + (jb % PPB)) * 1024 + lane * 16;
+      dst[i] = A_BYTES + jb * 1024;
+      step[i] = PPB * 1024;
+    }
+  }
+  auto issue = [&](int kt, int slot, int i0, int i1) {
+#pragma unroll
+    for (int i = 0; i < NPW; ++i)
+      if (i >= i0 && i < i1)
+        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)kt * step[i]),
+                                         (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+  };
+
+  int col[TN];
+  uint32_t zpx[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
-    csc[t] = ep_args.a_scale * wscale[col[t]];
-    cb[t] = bias ? bias[col[t]] : 0.0f;
+    col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+    const uint32_t zw = qzeros[col[t] >> 3];
+    zpx[t] = (((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u) * 0x01010101u;
   }
-  constexpr int EP_BYTES = 32 * WN * 4;
-  static_assert(NW * EP_BYTES <= STAGES * STAGE, "epilogue staging does not fit the LDS ring");
-  __syncthreads();
-  float* ep = (float*)(smem + wave * EP_BYTES);
-  const int row_base = m0 + wm * WM;
-  const int col_base = n0 + wn * WN;
-  constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
-  const float inv_out = ep_args.out_scale > 0.f ? 1.0f / ep_args.out_scale : 0.f;   // q8_exact (common.h)
-  const float inv_mid = ep_args.mid_scale > 0.f ? 1.0f / ep_args.mid_scale : 0.f;
+  int16_t_v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+  const int hsel = lane >> 5;
+  int a_off[TM], a_swz[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
-#pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        float v = (float)acc[i][t][r] * csc[t] + cb[t];
-        if (GELU) v = gelu_fast(v);
-        ep[rl * WN + t * 32 + (lane & 31)] = v;
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
-      constexpr int C4 = WN / 4;
-#pragma unroll
-      for (int j = 0; j < 32 * C4 / 64; ++j) {
-        const int idx = j * 64 + lane;
-        const int rl = idx / C4, c4 = idx % C4;
-        const int row = row_base + i * 32 + rl;
-        const float4_t v = ((const float4_t*)ep)[idx];
-        if (row < M) {
-          float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
-          if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
-        }
-      }
-    } else if (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) {
-      constexpr int C8 = WN / 8;
-#pragma unroll
-      for (int j = 0; j < (32 * C8 + 63) / 64; ++j) {
-        const int idx = j * 64 + lane;
-        if (idx < 32 * C8) {
-          const int rl = idx / C8, c8 = idx % C8;
-          const int row = row_base + i * 32 + rl;
-          const float4_t v0 = ((const float4_t*)ep)[2 * idx];
-          const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
-          if (row < M) {
-            const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
-                               (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
-            *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
-          }
-        }
-      }
-    } else {   // int8 codes, 16 columns per lane-store
-      constexpr int C16 = WN / 16;
-#pragma unroll
-      for (int j = 0; j < (32 * C16 + 63) / 64; ++j) {
-        const int idx = j * 64 + lane;
-        if (idx < 32 * C16) {
-          const int rl = idx / C16, c16 = idx % C16;
-          const int row = row_base + i * 32 + rl;
-          if (row < M) {
-            float v[16];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float4_t f = ((const float4_t*)ep)[4 * idx + e];
-              v[4 * e] = f[0]; v[4 * e + 1] = f[1]; v[4 * e + 2] = f[2]; v[4 * e + 3] = f[3];
-            }
-            u32x4 res;
-            if (EPI == SAMQ_EPI_Q8_RES)
-              res = *(const u32x4*)(ep_args.R + (int64_t)(ep_args.rmod > 0 ? row % ep_args.rmod : row) * ep_args.ldr +
-                                    col_base + 16 * c16);
-            u32x4 o;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-              uint32_t word = 0;
-#pragma unroll
-              for (int b = 0; b < 4; ++b) {
-                float x = v[4 * w + b];
-                if (EPI == SAMQ_EPI_Q8_RES) {
-                  if (ep_args.mid_scale > 0.f) x = q8_exact(x, ep_args.mid_scale, inv_mid) * ep_args.mid_scale;
-                  const float rv = (float)(int8_t)((res[w] >> (8 * b)) & 0xFFu) * ep_args.res_scale;
-                  x = rv + x;
-                }
-                const int qv = (int)q8_exact(x, ep_args.out_scale, inv_out);
-                word |= ((uint32_t)qv & 0xFFu) << (8 * b);
-              }
-              o[w] = word;
-            }
-            *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_off[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
   }
+  uint32_t kLo = 0x0F0F0F0Fu;
+  asm volatile("" : "+v"(kLo));
+
+  // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
+  const int pro = kt_count < LA ? kt_count : LA;
+#pragma unroll
+  for (int j = 0; j < LA; ++j)
+    if (j < pro) issue(j, j, 0, NPW);
+  i8_vm_wait_le<(LA - 1) * NPW>((pro - 1) * NPW);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  int slot = 0;
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const char* st = smem + slot * STAGE;
+    const int ahead = kt + LA;
+    const bool pf = ahead < kt_count && !(VAR & 4);
+    const int sa = slot + LA >= STAGES ? slot + LA - STAGES : slot + LA;   // (kt + LA) % STAGES
+#pragma unroll
+    for (int p = 0; p < NPH; ++p) {
+      // ---------------- load half
+      if (p == NPH - 1 && kt + 1 < kt_count) {
+        // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
+        int newer = pf ? PRE_LAST : 0;
+#pragma unroll
+        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
+        i8_vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+      }
+      u32x4 bw[TN];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bw[t] = *(const u32x4*)(st + A_BYTES + ((wn * TN + t) * PPB + p) * 1024 + lane * 16);
+      int4_t af[TM][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *(const int4_t*)(st + a_off[i] + (((2 * (2 * p + s) + hsel) ^ a_swz[i]) << 4));
+      int4_t bf[TN][2];
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const uint32_t w0 = bw[t][2 * s], w1 = bw[t][2 * s + 1];
+          if (VAR & 1) {
+            bf[t][s] = int4_t{(int)(w0 & kLo), (int)((w0 >> 4) & kLo), (int)(w1 & kLo), (int)((w1 >> 4) & kLo)};
+            continue;
+          }
+          bf[t][s][0] = w4_to_i8(w0 & kLo, zpx[t]);
+          bf[t][s][1] = w4_to_i8((w0 >> 4) & kLo, zpx[t]);
+          bf[t][s][2] = w4_to_i8(w1 & kLo, zpx[t]);
+          bf[t][s][3] = w4_to_i8((w1 >> 4) & kLo, zpx[t]);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---------------- MFMA half
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int t = 0; t < TN; ++t) {
+            if (VAR & 2) acc[i][t][0] += af[i][s][0] ^ bf[t][s][1];
+            else acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+          }
+      if (pf) issue(ahead, sa, i8_pre(p, NPW, NPH), i8_pre(p + 1, NPW, NPH));
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    slot = slot == STAGES - 1 ? 0 : slot + 1;
+  }
+  if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
+
+  __syncthreads();
+  i8_epilogue<TM, TN, WN, EPI>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * EP_BYTES), Cout, ldc, M,
+                               m0 + wm * WM, n0 + wn * WN, lane);
 }
 
 struct I8Args {
@@ -362,10 +571,32 @@ static int launch_i8(const I8Args& a, hipStream_t st) {
   return SAMQ_OK;
 }
 
-// tile configs: 81 256x256 (W4: 3 stages; W8: 2), 82 128x256, 83 128x128, 84 64x64
+template <int EPI, int STAGES, int LA, int VAR = 0>
+static int launch_i8_pp2(const I8Args& a, hipStream_t st) {
+  const int nwg = ((a.M + 255) / 256) * (a.N / 256);
+  hipLaunchKernelGGL((i8_gemm_pp2<EPI, STAGES, LA, VAR>), dim3(nwg), dim3(512), 0, st, a.A, a.lda, a.Wp, a.wscale,
+                     a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep);
+  SAMQ_LAUNCH_CHECK("i8_gemm_pp2 launch");
+  return SAMQ_OK;
+}
+
+// tile configs: 81 256x256 (W4: 3 stages; W8: 2), 82 128x256, 83 128x128, 84 64x64;
+// 85 the W4 ping-pong kernel (256x256, 3-slot ring, lookahead 2)
 template <int EPI, int BF>
 static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
   switch (cfg) {
+    case 85:
+      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2>(a, st);
+      else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 85 is the W4 ping-pong kernel");
+#ifdef SAMQ_TUNING
+    case 95: case 96: case 97:   // timing-only (wrong results): no zero point / no MFMA / no restaging
+      if constexpr (BF == BF_W4) {
+        if (cfg == 95) return launch_i8_pp2<EPI, 3, 2, 1>(a, st);
+        if (cfg == 96) return launch_i8_pp2<EPI, 3, 2, 2>(a, st);
+        return launch_i8_pp2<EPI, 3, 2, 4>(a, st);
+      }
+      return fail(SAMQ_ERR_INVALID, "i8_gemm: W4 only");
+#endif
     case 81:
       if constexpr (BF == BF_W4) return launch_i8<256, 256, 2, 4, EPI, BF, 3>(a, st);
       else return launch_i8<256, 256, 2, 4, EPI, BF, 2>(a, st);
@@ -377,7 +608,7 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: return 256; case 83: return 128; case 84: return 64; default: return 0; }
+  switch (cfg) { case 81: case 82: case 85: case 95: case 96: case 97: return 256; case 83: return 128; case 84: return 64; default: return 0; }
 }
 
 static int i8_pick_cfg(int M, int N, int bfmt) {
@@ -387,8 +618,10 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
   // tails -- proj / lin2 on them take the step 40.06 -> 38.29 ms, bit-identical
   // (tools/bench_cfg_ab_w4a8.py, profiles/r2_cfg_ab_w4a8.log); the round-1 pick of 128x128 for
   // N = 1280 came from isolated M = 16384 launches (profiles/r1_v11_i8_scan.log).
+  // Round 2: the ping-pong kernel (cfg 85) for those 256x256 tiles -- steady state 1759.7 -> 1663.3 us
+  // per ViT-H block at M = 65536, in the 2-lane W4A8 graph 37.46 -> 36.79 ms, bit-identical
   if (bfmt == BF_W4 && M >= 8192) {
-    if (N % 256 == 0) return 81;
+    if (N % 256 == 0) return 85;
     if (N % 128 == 0) return 83;
   }
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);

@@ -15,8 +15,8 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"pick": {}, "proj=81,lin2=81": {"proj": 81, "lin2": 81}, "proj=82,lin2=82": {"proj": 82, "lin2": 82},
-            "qkv=82,lin1=82": {"qkv": 82, "lin1": 82}, "proj=84,lin2=84": {"proj": 84, "lin2": 84}}
+VARIANTS = {"pick": {}, "all=85": {"qkv": 85, "proj": 85, "lin1": 85, "lin2": 85},
+            "qkv=85,lin2=85": {"qkv": 85, "lin2": 85}, "proj=85,lin1=85": {"proj": 85, "lin1": 85}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 enc.half()
