@@ -76,11 +76,14 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
 // y = float(acc) * (a_scale * wscale[n]) + bias[n] (-> GELU / residual / int8 quantiser), staged
 // through LDS in 32-row slices per wave (ep = this wave's 32 x WN f32 slice) so the global traffic
 // is row-contiguous 16-byte vectors.  Shared by the v3-style and the ping-pong int8 kernels.
-template <int TM, int TN, int WN, int EPI>
+// ZPS: the sums exclude the zero point (acc = sum a * q) and the epilogue subtracts zp[n] * S[m]
+// (zpv = this lane's zp per column block, ssum = S of the wave's WM rows; int32-exact)
+template <int TM, int TN, int WN, int EPI, bool ZPS = false>
 __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], const int (&col)[TN],
                                             const float* __restrict__ wscale, const float* __restrict__ bias,
                                             const I8Epi& ep_args, float* ep, void* __restrict__ Cout, int64_t ldc,
-                                            int M, int row_base, int col_base, int lane) {
+                                            int M, int row_base, int col_base, int lane,
+                                            const int* ssum = nullptr, const int* zpv = nullptr) {
   const int hsel = lane >> 5;
   float csc[TN], cb[TN];
 #pragma unroll
@@ -98,7 +101,9 @@ __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], cons
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        float v = (float)acc[i][t][r] * csc[t] + cb[t];
+        int a = acc[i][t][r];
+        if constexpr (ZPS) a -= zpv[t] * ssum[i * 32 + rl];
+        float v = (float)a * csc[t] + cb[t];
         if (GELU) v = gelu_fast(v);
         ep[rl * WN + t * 32 + (lane & 31)] = v;
       }
@@ -381,6 +386,11 @@ __device__ __forceinline__ void i8_vm_wait_le(int n) {   // s_waitcnt vmcnt(n) f
   }
 }
 
+// VAR & 8 (product, cfg 86): zero point by row sums -- the MFMA multiplies the raw nibbles q (an
+// AND per 4 weights instead of OR / SUB / XOR on top) and the epilogue subtracts zp[n] * S[m] with
+// S[m] = sum_k a[m, k] accumulated from the staged A tile by v_dot4 against ones (wave wn sums the
+// 32 rows of its M block wn, 8 dot4 + 2 LDS reads per phase; the 4 waves of an M half share the
+// sums through LDS at the end).  Integer-exact: identical outputs.
 // VAR (tuning build only, timing experiments that compute wrong results): 1 no zero-point
 // subtraction in the unpack, 2 no MFMA, 4 no restaging
 template <int EPI, int STAGES, int LA, int VAR = 0>
@@ -404,7 +414,7 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
   static_assert(LA >= 2 && LA < STAGES, "ring");
   static_assert((LA - 2) * NPW + PRE_LAST <= 63 && (LA - 1) * NPW <= 63, "vmcnt");
-  static_assert(SMEM <= 160 * 1024, "LDS");
+  static_assert(SMEM <= 160 * 1024 && NW * EP_BYTES + BM * 4 <= SMEM, "LDS");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -477,6 +487,11 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   }
   uint32_t kLo = 0x0F0F0F0Fu;
   asm volatile("" : "+v"(kLo));
+  constexpr bool ZPS = (VAR & 8) != 0;
+  static_assert(!ZPS || TM == WAVES_N, "row sums: wave wn sums M block wn");
+  const int rs_row = wm * WM + wn * 32 + (lane & 31);
+  const int rs_off = rs_row * ROWB, rs_swz = (rs_row >> 1) & 7;
+  int rsum = 0;
 
   // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
   const int pro = kt_count < LA ? kt_count : LA;
@@ -513,13 +528,21 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
 #pragma unroll
         for (int s = 0; s < 2; ++s)
           af[i][s] = *(const int4_t*)(st + a_off[i] + (((2 * (2 * p + s) + hsel) ^ a_swz[i]) << 4));
+      if constexpr (ZPS) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int4_t x = *(const int4_t*)(st + rs_off + (((2 * (2 * p + s) + hsel) ^ rs_swz) << 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rsum = __builtin_amdgcn_sdot4(x[e], 0x01010101, rsum, false);
+        }
+      }
       int4_t bf[TN][2];
 #pragma unroll
       for (int t = 0; t < TN; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const uint32_t w0 = bw[t][2 * s], w1 = bw[t][2 * s + 1];
-          if (VAR & 1) {
+          if ((VAR & 1) || ZPS) {
             bf[t][s] = int4_t{(int)(w0 & kLo), (int)((w0 >> 4) & kLo), (int)(w1 & kLo), (int)((w1 >> 4) & kLo)};
             continue;
           }
@@ -553,6 +576,18 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
 
   __syncthreads();
+  if constexpr (ZPS) {
+    int* s_lds = (int*)(smem + NW * EP_BYTES);
+    rsum += __shfl_xor(rsum, 32, 64);   // the two k halves of the row
+    if (lane < 32) s_lds[rs_row] = rsum;
+    __syncthreads();
+    int zpv[TN];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) zpv[t] = (int)(zpx[t] & 0xFFu);
+    i8_epilogue<TM, TN, WN, EPI, true>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * EP_BYTES), Cout,
+                                       ldc, M, m0 + wm * WM, n0 + wn * WN, lane, s_lds + wm * WM, zpv);
+    return;
+  }
   i8_epilogue<TM, TN, WN, EPI>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * EP_BYTES), Cout, ldc, M,
                                m0 + wm * WM, n0 + wn * WN, lane);
 }
@@ -588,6 +623,9 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 85:
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 85 is the W4 ping-pong kernel");
+    case 86:
+      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8>(a, st);
+      else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 86 is the W4 ping-pong kernel");
 #ifdef SAMQ_TUNING
     case 95: case 96: case 97:   // timing-only (wrong results): no zero point / no MFMA / no restaging
       if constexpr (BF == BF_W4) {
@@ -608,7 +646,7 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 95: case 96: case 97: return 256; case 83: return 128; case 84: return 64; default: return 0; }
+  switch (cfg) { case 81: case 82: case 85: case 86: case 95: case 96: case 97: return 256; case 83: return 128; case 84: return 64; default: return 0; }
 }
 
 static int i8_pick_cfg(int M, int N, int bfmt) {
@@ -618,10 +656,12 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
   // tails -- proj / lin2 on them take the step 40.06 -> 38.29 ms, bit-identical
   // (tools/bench_cfg_ab_w4a8.py, profiles/r2_cfg_ab_w4a8.log); the round-1 pick of 128x128 for
   // N = 1280 came from isolated M = 16384 launches (profiles/r1_v11_i8_scan.log).
-  // Round 2: the ping-pong kernel (cfg 85) for those 256x256 tiles -- steady state 1759.7 -> 1663.3 us
-  // per ViT-H block at M = 65536, in the 2-lane W4A8 graph 37.46 -> 36.79 ms, bit-identical
+  // Round 2: the ping-pong kernel for those 256x256 tiles, zero point through row sums (cfg 86): in
+  // the 2-lane W4A8 graph (interleaved A/B, tools/bench_cfg_ab_w4a8.py) 37.64 vs 38.33 ms for cfg
+  // 81 and 38.34 for cfg 85 (its plain-unpack form; steady state 1710 vs 1760 us per block for 81),
+  // bit-identical
   if (bfmt == BF_W4 && M >= 8192) {
-    if (N % 256 == 0) return 85;
+    if (N % 256 == 0) return 86;
     if (N % 128 == 0) return 83;
   }
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);

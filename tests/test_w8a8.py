@@ -118,7 +118,7 @@ def test_w8a8_gemm_epilogues(cuda, cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 85])
+@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 85, 86])
 def test_w4a8_gemm_exact_integer(cuda, cfg):
     """int4 (layout 3, incl. a zero point of 0 -> quirk 4) x int8: integer sums are exact."""
     from oracle import gptq_pack
@@ -151,19 +151,25 @@ def test_w4a8_gemm_exact_integer(cuda, cfg):
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,n", [(300, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280), (77, 128, 256),
                                    (260, 256, 768)])
-def test_w4a8_pingpong_matches_v3(cuda, m, k, n):
-    """The W4A8 ping-pong kernel (cfg 85) against the v3-style 256x256 kernel (cfg 81): both sum the
-    same int32 products exactly and share the epilogue code, so every epilogue must agree BIT FOR BIT
-    -- ragged M, K = 128 (one K tile, shorter than the lookahead), K = 256 (= the lookahead), and the
-    lin2 depth K = 5120."""
+@pytest.mark.parametrize("cfg", [85, 86])
+def test_w4a8_pingpong_matches_v3(cuda, m, k, n, cfg):
+    """The W4A8 ping-pong kernels (cfg 85; cfg 86 = zero point applied through per-row sums of the
+    int8 activations) against the v3-style 256x256 kernel (cfg 81): all sum the same int32 products
+    exactly and share the epilogue code, so every epilogue must agree BIT FOR BIT -- ragged M,
+    K = 128 (one K tile, shorter than the lookahead), K = 256 (= the lookahead), and the lin2 depth
+    K = 5120.  The weights include zero points of 0..15 (nibble + 1 = 1..16) and saturated codes."""
     from oracle import gptq_pack
     from samq import ops
     rng = np.random.Generator(np.random.PCG64(m + k + n))
     w = rng.standard_normal((n, k), dtype=np.float32) * np.float32(0.02)
+    w[7] = np.abs(w[7])   # an all-positive column: zero point nibble 0 (quirk 4)
     fake, s, z = gptq_pack.rtn_quantize_linear(w, -1)
     qw, qz, sc = gptq_pack.pack_linear(fake, s, z, -1)
     packed = ops.w4_repack(torch.from_numpy(qw).to(cuda), layout=3)
-    a = torch.from_numpy(rng.integers(-128, 128, (m, k), dtype=np.int8)).to(cuda)
+    a_np = rng.integers(-128, 128, (m, k), dtype=np.int8)
+    a_np[:3] = 127     # saturated rows: the largest row sums
+    a_np[3:5] = -128
+    a = torch.from_numpy(a_np).to(cuda)
     scf = torch.from_numpy(sc.astype(np.float32).reshape(-1)).to(cuda)
     qzd = torch.from_numpy(qz).to(cuda)
     bias = torch.from_numpy(rng.standard_normal(n, dtype=np.float32) * np.float32(0.02)).to(cuda)
@@ -171,12 +177,12 @@ def test_w4a8_pingpong_matches_v3(cuda, m, k, n):
     for epi, osc in ((ops.EPI_BIAS, 0.0), (ops.EPI_BIAS_GELU, 0.0), (ops.EPI_F32, 0.0), (ops.EPI_Q8, 0.05),
                      (ops.EPI_Q8_GELU, 0.03)):
         ref = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, a_s, osc, cfg=81)
-        got = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, a_s, osc, cfg=85)
+        got = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, a_s, osc, cfg=cfg)
         assert torch.equal(got, ref), f"epilogue {epi}"
     res0 = torch.from_numpy(rng.standard_normal((m, n), dtype=np.float32)).to(cuda)
     r81, r85 = res0.clone(), res0.clone()
     ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_RESADD_F32, a_s, out=r81, cfg=81)
-    ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_RESADD_F32, a_s, out=r85, cfg=85)
+    ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_RESADD_F32, a_s, out=r85, cfg=cfg)
     assert torch.equal(r85, r81)
 
 

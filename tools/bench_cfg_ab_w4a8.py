@@ -15,8 +15,8 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"pick": {}, "all=85": {"qkv": 85, "proj": 85, "lin1": 85, "lin2": 85},
-            "qkv=85,lin2=85": {"qkv": 85, "lin2": 85}, "proj=85,lin1=85": {"proj": 85, "lin1": 85}}
+VARIANTS = {"pick": {}, "all=86": {"qkv": 86, "proj": 86, "lin1": 86, "lin2": 86},
+            "all=81": {"qkv": 81, "proj": 81, "lin1": 81, "lin2": 81}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 enc.half()
