@@ -215,6 +215,14 @@ int samq_rel_attention(const void* qkv, const void* qkv_bias, const void* rel_po
                        const void* rel_pos_w, void* out, int B, int H, int W, int heads, int hd,
                        int window, float sm_scale, hipStream_t stream);
 
+/* samq_rel_attention with the W4A8 proj input quantiser folded into its store: out int8
+ * [B, H, W, heads*hd] = clamp(rne(fp16(o) / out_scale), -128, 127) -- the fq_vit QAct on the
+ * QuantLinear input (fq_vit/models/ptq/layers.py:203-242, quantizer/uniform.py:31-36) applied to
+ * the fp16 attention output, bit-identical to samq_rel_attention + samq_quantize.  out_scale > 0. */
+int samq_rel_attention_q(const void* qkv, const void* qkv_bias, const void* rel_pos_h,
+                         const void* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
+                         int window, float sm_scale, float out_scale, hipStream_t stream);
+
 /* Reference functional API `fused_attention.forward(inp, pos_emb1, pos_emb2, head_num,
  * hidden_dim, sm_scale)` (gptq_triton/fused_attention.py:312-358): attention over each of B
  * independent S x S grids with PRECOMPUTED bias terms rel_h, rel_w f16 [B*heads, S, S, S]

@@ -56,7 +56,23 @@ struct AttnParams {
   int nwx, upi;             // windows per row, windows per image
   float scale;              // sm_scale
   int nqb, units;           // streaming path with a 1-D XCD-ordered grid: query blocks, units
+  float out_scale, out_inv; // > 0: out holds int8 codes q8(fp16(o), out_scale) (W4A8 proj QAct)
 };
+
+// Store 4 output channels at element offset off of the [B, H, W, C] output: fp16, or (W4A8) the
+// int8 codes of the proj input QAct applied to the fp16-rounded value -- bit-identical to an fp16
+// store followed by samq_quantize, without the fp16 round trip through HBM.
+__device__ __forceinline__ void attn_store4(const AttnParams& p, int64_t off, float4_t o) {
+  const half4_t h = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
+  if (p.out_scale > 0.f) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)q8_exact((float)h[e], p.out_scale, p.out_inv) & 0xFFu) << (8 * e);
+    *(uint32_t*)((int8_t*)p.out + off) = w;
+  } else {
+    *(half4_t*)(p.out + off) = h;
+  }
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -481,14 +497,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
     const int x = qcol0[t] + ql;
     if (tok_kind(qrow[t], x) != 0) continue;
     const float inv = 1.0f / lt;
-    _Float16* dst = p.out + (((int64_t)b * p.H + (Y0 + qrow[t])) * p.W + (X0 + x)) * C + head * D;
+    const int64_t dst = (((int64_t)b * p.H + (Y0 + qrow[t])) * p.W + (X0 + x)) * C + head * D;
 #pragma unroll
-    for (int d = 0; d < DT; ++d) {
-      half4_t v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (_Float16)(o[t][d][r] * inv);
-      *(half4_t*)(dst + d * 16 + 4 * g) = v;
-    }
+    for (int d = 0; d < DT; ++d) attn_store4(p, dst + d * 16 + 4 * g, o[t][d] * inv);
   }
 }
 
@@ -780,14 +791,9 @@ struct Win {
       const int r = row0 + t;
       if (r >= G.nrow || ql >= G.ncol) continue;
       const float inv = __builtin_amdgcn_rcpf(lsum[t][0]);
-      _Float16* dst = p.out + (((int64_t)G.b * p.H + (G.Y0 + r)) * p.W + (G.X0 + ql)) * p.C + G.head * D;
+      const int64_t dst = (((int64_t)G.b * p.H + (G.Y0 + r)) * p.W + (G.X0 + ql)) * p.C + G.head * D;
 #pragma unroll
-      for (int d = 0; d < DT; ++d) {
-        half4_t v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)(o[t][d][e] * inv);
-        *(half4_t*)(dst + d * 16 + 4 * g) = v;
-      }
+      for (int d = 0; d < DT; ++d) attn_store4(p, dst + d * 16 + 4 * g, o[t][d] * inv);
     }
   }
 };
@@ -875,9 +881,9 @@ static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t str
 
 using namespace samq;
 
-extern "C" int samq_rel_attention(const void* qkv, const void* qkv_bias, const void* rel_pos_h, const void* rel_pos_w,
-                                  void* out, int B, int H, int W, int heads, int hd, int window, float sm_scale,
-                                  hipStream_t stream) {
+static int rel_attention_impl(const void* qkv, const void* qkv_bias, const void* rel_pos_h, const void* rel_pos_w,
+                              void* out, int B, int H, int W, int heads, int hd, int window, float sm_scale,
+                              float out_scale, hipStream_t stream) {
   SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention: null pointer");
   SAMQ_REQUIRE(hd == 64 || hd == 80, SAMQ_ERR_UNSUPPORTED, "rel_attention: head_dim must be 64 or 80");
   SAMQ_REQUIRE(B > 0 && H > 0 && W > 0 && heads > 0, SAMQ_ERR_INVALID, "rel_attention: bad shape");
@@ -893,6 +899,8 @@ extern "C" int samq_rel_attention(const void* qkv, const void* qkv_bias, const v
   p.H = H;
   p.W = W;
   p.scale = sm_scale;
+  p.out_scale = out_scale;
+  p.out_inv = out_scale > 0.f ? 1.0f / out_scale : 0.f;
   int units;
   if (window > 0) {
     SAMQ_REQUIRE(window <= 16, SAMQ_ERR_UNSUPPORTED, "rel_attention: window must be <= 16");
@@ -912,6 +920,22 @@ extern "C" int samq_rel_attention(const void* qkv, const void* qkv_bias, const v
   }
   SAMQ_REQUIRE(units <= 65535, SAMQ_ERR_INVALID, "rel_attention: too many windows*batch");
   return dispatch_attn<false>(p, hd, units, stream);
+}
+
+extern "C" int samq_rel_attention(const void* qkv, const void* qkv_bias, const void* rel_pos_h, const void* rel_pos_w,
+                                  void* out, int B, int H, int W, int heads, int hd, int window, float sm_scale,
+                                  hipStream_t stream) {
+  return rel_attention_impl(qkv, qkv_bias, rel_pos_h, rel_pos_w, out, B, H, W, heads, hd, window, sm_scale, 0.f,
+                            stream);
+}
+
+extern "C" int samq_rel_attention_q(const void* qkv, const void* qkv_bias, const void* rel_pos_h,
+                                    const void* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
+                                    int window, float sm_scale, float out_scale, hipStream_t stream) {
+  SAMQ_REQUIRE(out_scale > 0.f, SAMQ_ERR_INVALID, "rel_attention_q: out_scale must be > 0");
+  SAMQ_REQUIRE(((uintptr_t)out & 3) == 0, SAMQ_ERR_INVALID, "rel_attention_q: out must be 4-byte aligned");
+  return rel_attention_impl(qkv, qkv_bias, rel_pos_h, rel_pos_w, out, B, H, W, heads, hd, window, sm_scale,
+                            out_scale, stream);
 }
 
 extern "C" int samq_attention_relbias(const void* inp, const void* rel_h, const void* rel_w, void* out, int B, int S,

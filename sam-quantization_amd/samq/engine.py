@@ -150,7 +150,7 @@ class EncoderEngine:
                 bufs.update(xn8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
                             att8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
                             hid8=torch.empty((b, g, g, hid), dtype=torch.int8, device=dev))
-                del bufs["xn"], bufs["hid"]
+                del bufs["xn"], bufs["hid"], bufs["att"]
             self._bufs[(b, lane)] = bufs
         return bufs
 
@@ -180,12 +180,11 @@ class EncoderEngine:
 
     def block_w4a8(self, p: _BlockPlan, bufs) -> None:
         """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded
-        into LN / the GELU epilogue / a quantiser after the attention), int8 MFMA GEMMs."""
-        x, xn8, qkv, att, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att"], bufs["att8"], bufs["hid8"]
+        into LN / the GELU epilogue / the attention's store), int8 MFMA GEMMs."""
+        x, xn8, qkv, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att8"], bufs["hid8"]
         ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
         p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
-        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
-        ops.quantize(att, p.s_proj, out=att8)
+        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8, out_scale=p.s_proj)
         p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
         ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
         p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)

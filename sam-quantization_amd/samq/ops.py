@@ -184,19 +184,26 @@ def conv3x3_nhwc(x: torch.Tensor, weight_tap_major: torch.Tensor, out: Optional[
 # ----------------------------------------------------------------------------- attention
 def rel_attention(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,
                   rel_pos_w: torch.Tensor, heads: int, window: int, sm_scale: float,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """qkv f16 (B, H, W, 3C) -> out f16 (B, H, W, C); windowed (window > 0) or global."""
+                  out: Optional[torch.Tensor] = None, out_scale: float = 0.0) -> torch.Tensor:
+    """qkv f16 (B, H, W, 3C) -> out f16 (B, H, W, C); windowed (window > 0) or global.
+    out_scale > 0: out int8 codes of the fp16 output quantised with out_scale (samq_rel_attention_q,
+    the W4A8 proj-input QAct folded into the store)."""
     _need_cuda(qkv, qkv_bias, rel_pos_h, rel_pos_w)
     b, h, w, c3 = qkv.shape
     c = c3 // 3
     hd = c // heads
     assert qkv.dtype == torch.float16 and qkv.is_contiguous()
     assert rel_pos_h.dtype == torch.float16 and rel_pos_w.dtype == torch.float16
+    odt = torch.int8 if out_scale > 0 else torch.float16
     if out is None:
-        out = torch.empty((b, h, w, c), dtype=torch.float16, device=qkv.device)
-    _lib.check(_lib.load().samq_rel_attention(_ptr(qkv), _ptr(qkv_bias), _ptr(rel_pos_h.contiguous()),
-                                              _ptr(rel_pos_w.contiguous()), _ptr(out), b, h, w, heads, hd, window,
-                                              float(sm_scale), _stream()), "rel_attention")
+        out = torch.empty((b, h, w, c), dtype=odt, device=qkv.device)
+    assert out.dtype == odt and out.is_contiguous()
+    args = (_ptr(qkv), _ptr(qkv_bias), _ptr(rel_pos_h.contiguous()), _ptr(rel_pos_w.contiguous()), _ptr(out),
+            b, h, w, heads, hd, window, float(sm_scale))
+    if out_scale > 0:
+        _lib.check(_lib.load().samq_rel_attention_q(*args, float(out_scale), _stream()), "rel_attention_q")
+    else:
+        _lib.check(_lib.load().samq_rel_attention(*args, _stream()), "rel_attention")
     return out
 
 

@@ -234,6 +234,29 @@ def test_rel_attention(cuda, b, h, w, heads, d, window):
     _close(out, ref, 2.5e-3)
 
 
+@pytest.mark.parametrize("b,h,w,heads,d,window", [
+    (2, 64, 64, 16, 80, 14),    # ViT-H windowed lane (two-workgroups-per-CU window kernel)
+    (2, 64, 64, 16, 80, 0),     # ViT-H global lane (streaming kernel)
+    (1, 20, 33, 3, 64, 14),     # ragged grid, vit_b head dim
+    (3, 16, 16, 2, 80, 0),      # resident small global grid
+])
+def test_rel_attention_q_out(cuda, b, h, w, heads, d, window):
+    """samq_rel_attention_q (the W4A8 proj-input QAct folded into the attention store) is BIT-IDENTICAL
+    to samq_rel_attention followed by samq_quantize, and the codes match the oracle's fake quant up
+    to the fp16 rounding of the attention output (+-1 code)."""
+    from samq import ops
+    qkv16, bq, rph, rpw, ref = _attn_case(b, h, w, heads, d, window, seed=7 + h + window)
+    args = (_dev(qkv16, cuda), _dev(bq, cuda), _dev(rph, cuda), _dev(rpw, cuda), heads, window, d ** -0.5)
+    s = 0.011
+    o16 = ops.rel_attention(*args)
+    want = ops.quantize(o16, s)
+    got = ops.rel_attention(*args, out_scale=s)
+    torch.cuda.synchronize()
+    assert got.dtype == torch.int8 and torch.equal(got, want)
+    codes = np.clip(np.rint(ref / np.float32(s)), -128, 127)
+    assert np.abs(got.cpu().numpy().astype(np.int32) - codes).max() <= 1
+
+
 @pytest.mark.parametrize("tag", ["win", "glob"])
 def test_attention_functional_and_module_vs_reference_golden(cuda, golden_dir, tag):
     import samq
