@@ -14,7 +14,8 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"pick": {}, "ln_rpw=1": {"ln_rpw": 1}, "ln_rpw=4": {"ln_rpw": 4}}
+VARIANTS = {"pick": {}, "proj=22": {"proj": 22}, "proj=22,lin2=22": {"proj": 22, "lin2": 22},
+            "proj=22,lin1=22": {"proj": 22, "lin1": 22}, "proj=25,lin1=25": {"proj": 25, "lin1": 25}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 eng = enc.engine()
