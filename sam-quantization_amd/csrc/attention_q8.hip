@@ -495,6 +495,222 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   }
 }
 
+// ------------------------------------------------------------------ windows (S <= 16), key rows of 16 slots
+// The windowed blocks of the W8A8 encoder (14 x 14 windows).  A workgroup = one (window, head), NWQ
+// waves x 16 queries (query t = 16 wave + ql -> (t / S, t % S)).  The keys are staged once with key
+// (kh, kw) in slot 16 kh + kw (slots kw >= S zero and masked), so a 16-key block is exactly one key
+// row: the height term is one value per block and the width term a fixed per-lane set (kw = 4 g + i,
+// registers) -- per score no index decode and no table reads, unlike the generic path above.
+// Scores, quantisers, softmax and P.V (hi + lo fp16, tr-read V, MFMA row sums) as the row64 kernel.
+template <int SW, int NWQ>
+__global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Params p) {
+  constexpr int SLOTS = 16 * SW, VP = QD + 8;
+  constexpr int NCH = (SW + 3) / 4;                        // chunks of up to 4 key rows (64 slots)
+  static_assert(SW <= 16 && NWQ * 16 >= SW * SW, "one window per workgroup");
+  __shared__ __attribute__((aligned(16))) int8_t k_lds[SLOTS * KPITCH];
+  __shared__ __attribute__((aligned(16))) _Float16 v_lds[(SLOTS + 32) * VP];   // + a zero tail for the last k32 step
+  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
+  __shared__ float rh_lds[NWQ][16 * (SW + 1)];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = lane >> 4;
+  const int ql = lane & 15;
+  const int C = p.C;
+  const int head = blockIdx.y;
+  const int per = p.nwh * p.nww;
+  const int b = blockIdx.x / per;
+  const int wy = (blockIdx.x % per) / p.nww;
+  const int wx = blockIdx.x % p.nww;
+  auto tok_ptr = [&](int ty, int tx, bool& inimg) -> const int8_t* {
+    const int y = wy * SW + ty, x = wx * SW + tx;
+    inimg = y < p.H && x < p.W;
+    return p.qkv + (((int64_t)b * p.H + y) * p.W + x) * (3 * C);
+  };
+
+  // ---- stage K codes and V (fp16, row-major) of every key slot; pad tokens = q8(qkv bias)
+  for (int u = tid; u < (SLOTS + 32) * 4; u += 64 * NWQ) {
+    const int slot = u >> 2, part = u & 3;
+    const int kh = slot >> 4, kw = slot & 15;
+    u32x4 kc = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
+    if (kh < SW && kw < SW) {
+      bool inimg;
+      const int8_t* tp = tok_ptr(kh, kw, inimg);
+      if (inimg) {
+        kc = *(const u32x4*)(tp + C + head * QD + part * 16);
+        vc = *(const u32x4*)(tp + 2 * C + head * QD + part * 16);
+      } else if (p.qkv_bias) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int kq = (int)aq8(p.qkv_bias[C + head * QD + part * 16 + e], p.s_qkv);
+          const int vq = (int)aq8(p.qkv_bias[2 * C + head * QD + part * 16 + e], p.s_qkv);
+          kc[e >> 2] |= ((uint32_t)kq & 0xFFu) << (8 * (e & 3));
+          vc[e >> 2] |= ((uint32_t)vq & 0xFFu) << (8 * (e & 3));
+        }
+      }
+    }
+    if (slot < SLOTS) *(u32x4*)(&k_lds[slot * KPITCH + part * 16]) = kc;
+    half8_t h0, h1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      h0[e] = (_Float16)(float)(int8_t)((vc[e >> 2] >> (8 * (e & 3))) & 0xFFu);
+      h1[e] = (_Float16)(float)(int8_t)((vc[2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
+    }
+    *(half8_t*)(&v_lds[slot * VP + part * 16]) = h0;
+    *(half8_t*)(&v_lds[slot * VP + part * 16 + 8]) = h1;
+  }
+
+  // ---- this wave's 16 queries and their rel-pos terms (fp32 dot products of the fake-quant q with
+  // the f32 tables, rows qy - k + S - 1 for both: quirk 1); rel_w for kw = 4 g + i into registers
+  const int qt = wave * 16 + ql;
+  const bool q_in = qt < SW * SW;
+  const int qy = q_in ? qt / SW : 0, qx = q_in ? qt % SW : 0;
+  bool q_ok = false;
+  int4v qfrag = {0, 0, 0, 0};
+  if (q_in) {
+    const int8_t* tp = tok_ptr(qy, qx, q_ok);
+    if (q_ok) {
+      qfrag = *(const int4v*)(tp + head * QD + g * 16);
+    } else if (p.qkv_bias) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int qq = (int)aq8(p.qkv_bias[head * QD + g * 16 + e], p.s_qkv);
+        qfrag[e >> 2] |= (qq & 0xFF) << (8 * (e & 3));
+      }
+    }
+  }
+  *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  auto reldot = [&](int ridx, float& ah, float& aw) {
+    const float* th = p.relh + (int64_t)ridx * QD;
+    const float* tw = p.relw + (int64_t)ridx * QD;
+    ah = 0.f;
+    aw = 0.f;
+#pragma unroll 1
+    for (int d4 = 0; d4 < QD / 16; ++d4) {
+      const u32x4 cw = *(const u32x4*)(&q_lds[wave][ql * KPITCH + d4 * 16]);
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
+        const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
+          ah = fmaf(qf, h4[e], ah);
+          aw = fmaf(qf, w4[e], aw);
+        }
+      }
+    }
+  };
+  float rwr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kk = 4 * g + i;   // key column of this lane's score i; also the key row for rel_h below
+    float ah = 0.f, aw = 0.f;
+    if (kk < SW) reldot(qy - kk + SW - 1, ah, aw);
+    rwr[i] = aw;
+    if (kk < SW) rh_lds[wave][ql * (SW + 1) + kk] = ah;
+  }
+  __syncthreads();   // K / V staged; this wave's rel_h rows visible
+  const float* rhq = &rh_lds[wave][ql * (SW + 1)];
+
+  const float c1 = p.qk_scale * p.inv_a1, sa1 = p.s_a1, inv2 = p.inv_a2, k2 = p.k2;
+  const int trow = ql >> 2, tcol = 4 * (ql & 3);
+  const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
+  float m = -INFINITY;
+  float4_t acc[QD / 16], lacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    constexpr int dummy = 0;
+    (void)dummy;
+    const int nb = SW - 4 * ch < 4 ? SW - 4 * ch : 4;   // key rows in this chunk (compile-time after unroll)
+    float c[4][4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      if (bb >= nb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) c[bb][i] = -INFINITY;
+        continue;
+      }
+      const int kh = 4 * ch + bb;
+      const float rh_row = rhq[kh];
+      const int4v kf = *(const int4v*)(&k_lds[(kh * 16 + ql) * KPITCH + g * 16]);
+      const int4v z = {0, 0, 0, 0};
+      const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f) * sa1;
+        const float t = (v1 + rh_row) + rwr[i];
+        const float cq = __builtin_amdgcn_fmed3f(__builtin_rintf(t * inv2), -128.f, 127.f);
+        c[bb][i] = 4 * g + i < SW ? cq : -INFINITY;
+      }
+    }
+    float cmax = q8max3(c[0][0], c[0][1], c[0][2]);
+    cmax = q8max3(cmax, c[0][3], c[1][0]);
+    cmax = q8max3(cmax, c[1][1], c[1][2]);
+    cmax = q8max3(cmax, c[1][3], c[2][0]);
+    cmax = q8max3(cmax, c[2][1], c[2][2]);
+    cmax = q8max3(cmax, c[2][3], c[3][0]);
+    cmax = q8max3(cmax, c[3][1], c[3][2]);
+    cmax = fmaxf(cmax, c[3][3]);
+    cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    if (cmax > m) {
+      const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
+      lacc = lacc * alpha;
+      m = cmax;
+    }
+    const float off = -m * k2;
+    const _Float16* vb = &v_lds[(ch * 64) * VP];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      if (2 * s2 >= nb) continue;   // both key rows of this k32 step are past the window
+      half8_t bhi, blo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float cv = c[2 * s2 + (j >> 2)][j & 3];
+        const float pv = cv == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(cv, k2, off));
+        const _Float16 h = (_Float16)pv;
+        bhi[j] = h;
+        blo[j] = (_Float16)(pv - (float)h);
+      }
+#pragma unroll
+      for (int t = 0; t < QD / 16; ++t) {
+        const _Float16* a0 = vb + (32 * s2 + 4 * g + trow) * VP + t * 16 + tcol;
+        const half4_t lo = __builtin_bit_cast(half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)a0));
+        const half4_t hi = __builtin_bit_cast(
+            half4_t, __builtin_amdgcn_ds_read_tr16_b64_v4i16((SAMQ_LDS short4_t*)(a0 + 16 * VP)));
+        const half8_t af = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, bhi, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af, blo, acc[t], 0, 0, 0);
+      }
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, bhi, lacc, 0, 0, 0);
+      lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, blo, lacc, 0, 0, 0);
+    }
+  }
+
+  if (q_ok) {
+    const float lsum = lacc[0];
+    int8_t* op = p.out + (((int64_t)b * p.H + (wy * SW + qy)) * p.W + (wx * SW + qx)) * C + head * QD;
+#pragma unroll
+    for (int t = 0; t < QD / 16; ++t) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float o = acc[t][i] / lsum * p.s_qkv;
+        w |= ((uint32_t)(int)aq8(o, p.s_out) & 0xFFu) << (8 * i);
+      }
+      *(uint32_t*)(op + t * 16 + 4 * g) = w;
+    }
+  }
+}
+
 }  // namespace samq
 
 using namespace samq;
@@ -523,7 +739,9 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.nwh = (H + window - 1) / window; p.nww = (W + window - 1) / window;
     p.L = window * window;
     const dim3 grid(B * p.nwh * p.nww, heads, 1);
-    if (p.L <= 13 * 16)   // SAM's 14 x 14 windows: 13 waves of 16 queries
+    if (window == 14)     // SAM's 14 x 14 windows: key rows of 16 slots, 13 waves of 16 queries
+      hipLaunchKernelGGL((rel_attention_q8_win_kernel<14, 13>), grid, dim3(64 * 13), 0, stream, p);
+    else if (p.L <= 13 * 16)
       hipLaunchKernelGGL((rel_attention_q8_kernel<true, 13, 256, 16>), grid, dim3(64 * 13), 0, stream, p);
     else
       hipLaunchKernelGGL((rel_attention_q8_kernel<true, 16, 256, 16>), grid, dim3(64 * 16), 0, stream, p);
