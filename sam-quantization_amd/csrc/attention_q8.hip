@@ -302,6 +302,45 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
 }
 
 
+// rel_h / rel_w for the 16 queries of a wave that share the query grid row qy, by MFMA:
+// rel[kk][q] = s_qkv * sum_d code_q[d] * R[qy - kk + side - 1][d], for the 16 key rows / columns
+// kk = 16 bb + m of block bb (A operand row m = the table row of kk; B = the int8 query codes,
+// exact in fp16); the f32 tables enter as fp16 hi + lo pairs (|R - hi - lo| <= 2^-22 |R|), so the
+// sums carry fp32-level error like a scalar fp32 dot product (whose order differs from the
+// reference's anyway).  Lane (ql, g) receives rel[16 bb + 4 g + i][query ql], i = 0..3.
+__device__ __forceinline__ void q8_rel_block(const AttnQ8Params& p, const int8_t* qcodes_lane, int qy, int side,
+                                             int bb, int lane, float4_t& rh4, float4_t& rw4) {
+  const int ql = lane & 15, g = lane >> 4;
+  int r = qy - (16 * bb + ql) + side - 1;      // table row of this lane's A row (kk = 16 bb + ql)
+  r = r < 0 ? 0 : (r > 2 * side - 2 ? 2 * side - 2 : r);   // rows past the window: any valid row (masked)
+  rh4 = float4_t{0.f, 0.f, 0.f, 0.f};
+  rw4 = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < QD / 32; ++s) {
+    const uint2 cw = *(const uint2*)(qcodes_lane + 32 * s + 8 * g);   // codes of query ql, dims 32s+8g..+7
+    half8_t qb;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qb[e] = (_Float16)(float)(int8_t)((((e < 4) ? cw.x : cw.y) >> (8 * (e & 3))) & 0xFFu);
+#pragma unroll
+    for (int tab = 0; tab < 2; ++tab) {
+      const float* src = (tab ? p.relw : p.relh) + (int64_t)r * QD + 32 * s + 8 * g;
+      const float4_t x0 = *(const float4_t*)src, x1 = *(const float4_t*)(src + 4);
+      half8_t hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x = e < 4 ? x0[e] : x1[e - 4];
+        hi[e] = (_Float16)x;
+        lo[e] = (_Float16)(x - (float)hi[e]);
+      }
+      float4_t& d = tab ? rw4 : rh4;
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, qb, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, qb, d, 0, 0, 0);
+    }
+  }
+  rh4 = rh4 * p.s_qkv;
+  rw4 = rw4 * p.s_qkv;
+}
+
 // ------------------------------------------------------------------ global, 64 x 64 grid (vit_b)
 // The global blocks of the W8A8 vit_b encoder (4096 keys).  A workgroup = one query grid row
 // (64 queries, 4 waves x 16); key row kh is chunk kh (64 keys): its K codes (int8) and V codes
@@ -378,32 +417,15 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   __builtin_amdgcn_s_waitcnt(0xC07F);
   float rwr[4][4];
 #pragma unroll
-  for (int bb = 0; bb < 4; ++bb)
+  for (int bb = 0; bb < 4; ++bb) {
+    float4_t rh4, rw4;
+    q8_rel_block(p, &q_lds[wave][ql * KPITCH], qy, G, bb, lane, rh4, rw4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int kk = 16 * bb + 4 * g + i;
-      const int ridx = qy - kk + G - 1;
-      const float* th = p.relh + (int64_t)ridx * QD;
-      const float* tw = p.relw + (int64_t)ridx * QD;
-      float ah = 0.f, aw = 0.f;
-#pragma unroll 1
-      for (int d4 = 0; d4 < QD / 16; ++d4) {
-        const u32x4 cw = *(const u32x4*)(&q_lds[wave][ql * KPITCH + d4 * 16]);
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
-          const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
-            ah = fmaf(qf, h4[e], ah);
-            aw = fmaf(qf, w4[e], aw);
-          }
-        }
-      }
-      rh_lds[wave][ql * (G + 1) + kk] = ah;
-      rwr[bb][i] = aw;
+      rh_lds[wave][ql * (G + 1) + 16 * bb + 4 * g + i] = rh4[i];
+      rwr[bb][i] = rw4[i];
     }
+  }
   store(0);
   __syncthreads();   // chunk 0 staged; the rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (G + 1)];
@@ -496,19 +518,20 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
 }
 
 // ------------------------------------------------------------------ windows (S <= 16), key rows of 16 slots
-// The windowed blocks of the W8A8 encoder (14 x 14 windows).  A workgroup = one (window, head), NWQ
-// waves x 16 queries (query t = 16 wave + ql -> (t / S, t % S)).  The keys are staged once with key
+// The windowed blocks of the W8A8 encoder (14 x 14 windows).  A workgroup = one (window, head), one
+// wave per query row (16 slots, query (wave, ql), slots ql >= S idle), so the rel-pos terms of a
+// wave are one MFMA block (q8_rel_block).  The keys are staged once with key
 // (kh, kw) in slot 16 kh + kw (slots kw >= S zero and masked), so a 16-key block is exactly one key
 // row: the height term is one value per block and the width term a fixed per-lane set (kw = 4 g + i,
 // registers) -- per score no index decode and no table reads, unlike the generic path above.
 // Scores, quantisers, softmax and P.V (hi + lo fp16, tr-read V, MFMA row sums) as the row64 kernel.
-template <int SW, int NWQ>
-__global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Params p) {
-  constexpr int SLOTS = 16 * SW, VP = QD + 8;
+template <int SW>
+__global__ __launch_bounds__(64 * SW, 2) void rel_attention_q8_win_kernel(AttnQ8Params p) {   // 2 per CU: LDS <= 80 KiB, <= 72 VGPRs
+  constexpr int NWQ = SW, SLOTS = 16 * SW, VP = QD + 8;
   constexpr int NCH = (SW + 3) / 4;                        // chunks of up to 4 key rows (64 slots)
-  static_assert(SW <= 16 && NWQ * 16 >= SW * SW, "one window per workgroup");
+  static_assert(SW <= 16, "one window per workgroup");
   __shared__ __attribute__((aligned(16))) int8_t k_lds[SLOTS * KPITCH];
-  __shared__ __attribute__((aligned(16))) _Float16 v_lds[(SLOTS + 32) * VP];   // + a zero tail for the last k32 step
+  __shared__ __attribute__((aligned(16))) _Float16 v_lds[SLOTS * VP];
   __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
   __shared__ float rh_lds[NWQ][16 * (SW + 1)];
 
@@ -530,7 +553,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Pa
   };
 
   // ---- stage K codes and V (fp16, row-major) of every key slot; pad tokens = q8(qkv bias)
-  for (int u = tid; u < (SLOTS + 32) * 4; u += 64 * NWQ) {
+  for (int u = tid; u < SLOTS * 4; u += 64 * NWQ) {
     const int slot = u >> 2, part = u & 3;
     const int kh = slot >> 4, kw = slot & 15;
     u32x4 kc = {0u, 0u, 0u, 0u}, vc = {0u, 0u, 0u, 0u};
@@ -550,7 +573,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Pa
         }
       }
     }
-    if (slot < SLOTS) *(u32x4*)(&k_lds[slot * KPITCH + part * 16]) = kc;
+    *(u32x4*)(&k_lds[slot * KPITCH + part * 16]) = kc;
     half8_t h0, h1;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -561,11 +584,10 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Pa
     *(half8_t*)(&v_lds[slot * VP + part * 16 + 8]) = h1;
   }
 
-  // ---- this wave's 16 queries and their rel-pos terms (fp32 dot products of the fake-quant q with
-  // the f32 tables, rows qy - k + S - 1 for both: quirk 1); rel_w for kw = 4 g + i into registers
-  const int qt = wave * 16 + ql;
-  const bool q_in = qt < SW * SW;
-  const int qy = q_in ? qt / SW : 0, qx = q_in ? qt % SW : 0;
+  // ---- this wave's query row qy = wave (queries qx = ql < S) and its rel-pos terms (MFMA, rows
+  // qy - k + S - 1 for both tables: quirk 1); rel_w for kw = 4 g + i into registers
+  const bool q_in = ql < SW;
+  const int qy = wave, qx = q_in ? ql : 0;
   bool q_ok = false;
   int4v qfrag = {0, 0, 0, 0};
   if (q_in) {
@@ -582,35 +604,15 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_win_kernel(AttnQ8Pa
   }
   *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
   __builtin_amdgcn_s_waitcnt(0xC07F);
-  auto reldot = [&](int ridx, float& ah, float& aw) {
-    const float* th = p.relh + (int64_t)ridx * QD;
-    const float* tw = p.relw + (int64_t)ridx * QD;
-    ah = 0.f;
-    aw = 0.f;
-#pragma unroll 1
-    for (int d4 = 0; d4 < QD / 16; ++d4) {
-      const u32x4 cw = *(const u32x4*)(&q_lds[wave][ql * KPITCH + d4 * 16]);
-#pragma unroll
-      for (int e4 = 0; e4 < 4; ++e4) {
-        const float4_t h4 = *(const float4_t*)(th + d4 * 16 + e4 * 4);
-        const float4_t w4 = *(const float4_t*)(tw + d4 * 16 + e4 * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float qf = (float)(int8_t)((cw[e4] >> (8 * e)) & 0xFFu) * p.s_qkv;
-          ah = fmaf(qf, h4[e], ah);
-          aw = fmaf(qf, w4[e], aw);
-        }
-      }
-    }
-  };
   float rwr[4];
+  {
+    float4_t rh4, rw4;
+    q8_rel_block(p, &q_lds[wave][ql * KPITCH], qy, SW, 0, lane, rh4, rw4);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int kk = 4 * g + i;   // key column of this lane's score i; also the key row for rel_h below
-    float ah = 0.f, aw = 0.f;
-    if (kk < SW) reldot(qy - kk + SW - 1, ah, aw);
-    rwr[i] = aw;
-    if (kk < SW) rh_lds[wave][ql * (SW + 1) + kk] = ah;
+    for (int i = 0; i < 4; ++i) {
+      rwr[i] = rw4[i];
+      if (4 * g + i < SW) rh_lds[wave][ql * (SW + 1) + 4 * g + i] = rh4[i];
+    }
   }
   __syncthreads();   // K / V staged; this wave's rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (SW + 1)];
@@ -739,8 +741,8 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.nwh = (H + window - 1) / window; p.nww = (W + window - 1) / window;
     p.L = window * window;
     const dim3 grid(B * p.nwh * p.nww, heads, 1);
-    if (window == 14)     // SAM's 14 x 14 windows: key rows of 16 slots, 13 waves of 16 queries
-      hipLaunchKernelGGL((rel_attention_q8_win_kernel<14, 13>), grid, dim3(64 * 13), 0, stream, p);
+    if (window == 14)     // SAM's 14 x 14 windows: key and query rows of 16 slots
+      hipLaunchKernelGGL((rel_attention_q8_win_kernel<14>), grid, dim3(64 * 14), 0, stream, p);
     else if (p.L <= 13 * 16)
       hipLaunchKernelGGL((rel_attention_q8_kernel<true, 13, 256, 16>), grid, dim3(64 * 13), 0, stream, p);
     else
