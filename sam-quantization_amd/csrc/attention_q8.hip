@@ -430,7 +430,16 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   __syncthreads();   // chunk 0 staged; the rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (G + 1)];
 
-  const float c1 = p.qk_scale * p.inv_a1, sa1 = p.s_a1, inv2 = p.inv_a2, k2 = p.k2;
+  // second quantiser argument (v1 + rel_h + rel_w) / s_a2 as fma(code1, s_a1 / s_a2, (rel_h + rel_w) /
+  // s_a2): 8 instead of 10 VALU per score (reciprocal-multiply quantisers: see rel_attention_q8_kernel)
+  const float c1 = p.qk_scale * p.inv_a1, inv2 = p.inv_a2, k2 = p.k2, k12 = p.s_a1 * p.inv_a2;
+#pragma unroll
+  for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rwr[bb][i] *= inv2;
+  // lazy softmax offset: m moves only when a code exceeds it by more than 8 / k2 (P <= 2^8, far
+  // inside fp16; O and l carry the same offset) -- most chunks then skip the O / l rescale
+  const float lazy = 8.0f / k2;
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
   float m = -INFINITY;
@@ -442,7 +451,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
     const int buf = ch & 1;
     if (ch + 1 < G) load(ch + 1);               // in flight under this chunk's math
     // ---- scores -> two quantisers -> integer codes c
-    const float rh_row = rhq[ch];
+    const float rh_row = rhq[ch] * inv2;
     float c[4][4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
@@ -451,9 +460,8 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
       const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float v1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f) * sa1;
-        const float t = (v1 + rh_row) + rwr[bb][i];
-        c[bb][i] = __builtin_amdgcn_fmed3f(__builtin_rintf(t * inv2), -128.f, 127.f);
+        const float q1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f);
+        c[bb][i] = __builtin_amdgcn_fmed3f(__builtin_rintf(fmaf(q1, k12, rh_row + rwr[bb][i])), -128.f, 127.f);
       }
     }
     float cmax = q8max3(c[0][0], c[0][1], c[0][2]);
@@ -466,7 +474,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
     cmax = fmaxf(cmax, c[3][3]);
     cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
     cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    if (cmax > m) {   // wave-uniform per query column: rescale O and l
+    if (cmax > m + lazy) {   // per query column: move the offset, rescale O and l
       const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
 #pragma unroll
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
@@ -526,7 +534,8 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
 // registers) -- per score no index decode and no table reads, unlike the generic path above.
 // Scores, quantisers, softmax and P.V (hi + lo fp16, tr-read V, MFMA row sums) as the row64 kernel.
 template <int SW>
-__global__ __launch_bounds__(64 * SW, 2) void rel_attention_q8_win_kernel(AttnQ8Params p) {   // 2 per CU: LDS <= 80 KiB, <= 72 VGPRs
+// two workgroups per CU: LDS <= 80 KiB and (HIP's second bound = waves per SIMD) <= 512 / 7 VGPRs
+__global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_win_kernel(AttnQ8Params p) {
   constexpr int NWQ = SW, SLOTS = 16 * SW, VP = QD + 8;
   constexpr int NCH = (SW + 3) / 4;                        // chunks of up to 4 key rows (64 slots)
   static_assert(SW <= 16, "one window per workgroup");
@@ -617,7 +626,10 @@ __global__ __launch_bounds__(64 * SW, 2) void rel_attention_q8_win_kernel(AttnQ8
   __syncthreads();   // K / V staged; this wave's rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (SW + 1)];
 
-  const float c1 = p.qk_scale * p.inv_a1, sa1 = p.s_a1, inv2 = p.inv_a2, k2 = p.k2;
+  const float c1 = p.qk_scale * p.inv_a1, inv2 = p.inv_a2, k2 = p.k2, k12 = p.s_a1 * p.inv_a2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rwr[i] *= inv2;   // see the row64 kernel
+  const float lazy = 8.0f / k2;
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
   float m = -INFINITY;
@@ -639,15 +651,14 @@ __global__ __launch_bounds__(64 * SW, 2) void rel_attention_q8_win_kernel(AttnQ8
         continue;
       }
       const int kh = 4 * ch + bb;
-      const float rh_row = rhq[kh];
+      const float rh_row = rhq[kh] * inv2;
       const int4v kf = *(const int4v*)(&k_lds[(kh * 16 + ql) * KPITCH + g * 16]);
       const int4v z = {0, 0, 0, 0};
       const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float v1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f) * sa1;
-        const float t = (v1 + rh_row) + rwr[i];
-        const float cq = __builtin_amdgcn_fmed3f(__builtin_rintf(t * inv2), -128.f, 127.f);
+        const float q1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f);
+        const float cq = __builtin_amdgcn_fmed3f(__builtin_rintf(fmaf(q1, k12, rh_row + rwr[i])), -128.f, 127.f);
         c[bb][i] = 4 * g + i < SW ? cq : -INFINITY;
       }
     }
@@ -661,7 +672,7 @@ __global__ __launch_bounds__(64 * SW, 2) void rel_attention_q8_win_kernel(AttnQ8
     cmax = fmaxf(cmax, c[3][3]);
     cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
     cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    if (cmax > m) {
+    if (cmax > m + lazy) {
       const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
 #pragma unroll
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
