@@ -148,6 +148,8 @@ def is_proj_gemm(mode, name):
     selects the int4-weight form, AG = 0 the plain row-major A operand (not the implicit convs)."""
     if mode == "w4a16":
         return "w4a16_gemm" in name
+    if mode == "w4a8" and "i8_gemm_pp2<" in name:   # the int4-weight ping-pong GEMM (M >= 8192)
+        return True
     if "i8_gemm_kernel<" not in name:
         return False
     args = [a.strip() for a in name.split("i8_gemm_kernel<", 1)[1].split(">", 1)[0].split(",")]
@@ -217,7 +219,7 @@ def w4a8_roofline(eng, batch: int):
     achieved = fl / t / 1e12
     return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_INT8_TOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_INT8_TOPS, 4), traffic=None,
-                kernel="i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)", launches_timed=n,
+                kernel="i8_gemm_pp2 / i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)", launches_timed=n,
                 avg_launch_us=round(t / n * 1e6, 2))
 
 
@@ -520,7 +522,7 @@ def main():
         alg_b = round(sum(alg) / len(alg))
     else:
         traffic, src, alg_b = None, None, None
-        kernel = ("i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)" if mode == "w4a8"
+        kernel = ("i8_gemm_pp2 / i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)" if mode == "w4a8"
                   else "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes + neck 1x1)")
     flops_step = gemm_flops_per_step(mode, eng, rows)
     live = dict(achieved=iso["achieved"], frac=iso["frac"], avg_launch_us=iso["avg_launch_us"],
