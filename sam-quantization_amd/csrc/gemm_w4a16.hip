@@ -905,7 +905,13 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // tile kt-1's last phase lie before it, and their lgkmcnt waits precede their MFMAs), so all
   // phases may restage (WAR).  The retire wait for tile kt+1 sits in the load half of the last
   // phase, before the barrier after which the first group reads it (RAW).
-  constexpr int PRE_LAST = pp2_pre(NPH - 1, NPW, NPH, 0);
+  // VAR & 32: all of tile kt+LA's pieces are issued in the LOAD half of tile kt's last phase,
+  // right after the retire wait for tile kt+1 and the phase's A fragment reads (the MFMA halves
+  // carry no DMA issue).  WAR: that segment starts two barriers after the partner group's
+  // lgkmcnt wait on its last reads of tile kt-1 (whose slot is restaged), so every read of the
+  // slot has completed.
+  constexpr bool DMA_LOAD = (VAR & 32) != 0;
+  constexpr int PRE_LAST = DMA_LOAD ? 0 : pp2_pre(NPH - 1, NPW, NPH, 0);
   // VAR & 16: v_mfma_f32_16x16x32_f16 fragments (same tile, LDS bytes and unpack count; the chip
   // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
   constexpr bool M16 = (VAR & 16) != 0;
@@ -1095,6 +1101,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
           for (int s = 0; s < KPP; ++s) bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
       }
+      if (DMA_LOAD && pf && p == NPH - 1) issue(ahead, sa, 0, NPW);
       if (VAR & 4) stamp(0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
@@ -1128,7 +1135,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       }
       // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
       // the barrier otherwise; WAR-safe in every phase: see header)
-      if (pf) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
+      if (pf && !DMA_LOAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
       if (VAR & 4) stamp(2);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
@@ -1231,6 +1238,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // wrong results on purpose -- never reachable through the product library
       case 60: return launch_pp2<1, 8, 1, 2, 4, 3, EPI>(a, st);   // 1x8 waves (256x32 each): B unpacked once
       case 61: return launch_pp2<1, 8, 1, 4, 4, 3, EPI>(a, st);   // 1x8 waves, 4 k-phases
+      // all LDS-DMA pieces in the last phase's load half instead of behind the MFMA bursts
+      // (measured: 57 -> 66 +1-3 %, 64 -> 67 within +-2 %, in-graph no change; DESIGN dead ends)
+      case 66: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 32>(a, st);
+      case 67: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 48>(a, st);
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1273,6 +1284,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
     case 11: return launch_cfg<256, 256, 2, 4, EPI, GR, 0>(a, st);   // literal-constant unpack (A/B)
     case 27: return launch_v3<128, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
     case 28: return launch_v3<256, 256, 2, 4, EPI, GR, 1>(a, st);   // timing-only: no unpack
+    // one wave per SIMD, 128x128 / 256x64 per wave (acc in the 512-register file): 10-20 %
+    // slower than the ping-pong cfg 57 on every shape (DESIGN dead ends)
+    case 32: return launch_v3<256, 256, 2, 2, EPI, GR>(a, st);
+    case 33: return launch_v3<256, 256, 1, 4, EPI, GR>(a, st);
     // v4 (16x16x32): needs weights repacked in LAYOUT 2 -- the caller's responsibility here
     case 41: return launch_v4<128, 256, 2, 4, EPI, GR>(a, st);
     case 42: return launch_v4<256, 256, 2, 4, EPI, GR>(a, st);
@@ -1313,10 +1328,10 @@ static int cfg_bn(int cfg) {
                  case 9: return 256; case 11: return 256; case 21: return 256; case 22: return 256;
                  case 23: return 128; case 24: return 128; case 25: return 256; case 26: return 64;
                  case 27: return 256; case 28: return 256; case 29: return 320; case 30: return 320;
-                 case 31: return 320; case 41: return 256; case 42: return 256;
+                 case 31: return 320; case 32: return 256; case 33: return 256; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
                  case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
-                 case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256;
+                 case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 66: return 256; case 67: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }
 }
@@ -1376,10 +1391,10 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
   const bool vec_ok = ((uintptr_t)C & 15) == 0 && ldc % 8 == 0;
   if (cfg <= 0) {
     cfg = pick_cfg(M, N, groupsize != -1 && groupsize != K);
-    if (!vec_ok && ((cfg >= 21 && cfg <= 31) || cfg >= 50)) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
+    if (!vec_ok && ((cfg >= 21 && cfg <= 33) || cfg >= 50)) cfg = N % 128 == 0 ? 3 : (N % 64 == 0 ? 4 : 5);
   }
   SAMQ_REQUIRE(cfg_bn(cfg) > 0 && N % cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a16_gemm: N not divisible by tile");
-  SAMQ_REQUIRE(vec_ok || ((cfg < 21 || cfg > 31) && cfg < 50), SAMQ_ERR_INVALID,
+  SAMQ_REQUIRE(vec_ok || ((cfg < 21 || cfg > 33) && cfg < 50), SAMQ_ERR_INVALID,
                "w4a16_gemm: this tile config needs a 16-byte aligned C with ldc % 8 == 0");
   GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
              (const _Float16*)bias, C, ldc, M, N, K, groupsize};

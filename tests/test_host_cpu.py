@@ -175,3 +175,28 @@ def test_w4_unpack_bit_trick_exact():
         lo, hi = f16(x & 0xFFFF) - magic, f16(x >> 16) - magic
         assert np.array_equal(lo, (w >> (4 * i)) & 15)
         assert np.array_equal(hi, (w >> (16 + 4 * i)) & 15)
+
+
+def test_bench_in_step_gemm_classifier_on_committed_profiles():
+    """bench.is_proj_gemm picks exactly the projection GEMMs out of every committed in-step kernel
+    trace (profiles/instep_*.json): the W4A8 int8 ping-pong GEMM (i8_gemm_pp2) included, attention /
+    LayerNorm / convolution kernels excluded, and each trace's GEMM union interval is non-empty."""
+    import json
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo))
+    import bench
+    files = sorted((repo / "profiles").glob("instep_*.json"))
+    assert files
+    for f in files:
+        mode = f.name.split("_")[1]
+        d = json.loads(f.read_text())
+        gemms = [k for k in d["kernels"] if bench.is_proj_gemm(mode, k)]
+        assert gemms, f.name
+        for k in d["kernels"]:
+            if any(t in k for t in ("attention", "layernorm", "conv_gemm", "patch_embed", "quantize")):
+                assert not bench.is_proj_gemm(mode, k), (f.name, k)
+        assert d["gemm_union_ns"] > 0, f.name
+    assert bench.is_proj_gemm("w4a8", "void samq::i8_gemm_pp2<5, 3, 2, 8>(signed char const*, long)")
+    assert not bench.is_proj_gemm("w8a8", "void samq::i8_gemm_pp2<5, 3, 2, 8>(signed char const*, long)")

@@ -16,6 +16,11 @@ lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 VARIANTS = {"pick": {}, "proj=22": {"proj": 22}, "proj=22,lin2=22": {"proj": 22, "lin2": 22},
             "proj=22,lin1=22": {"proj": 22, "lin1": 22}, "proj=25,lin1=25": {"proj": 25, "lin1": 25}}
+if len(sys.argv) > 3:   # variants as "name:layer=cfg,layer=cfg;name:..." (pick always first)
+    VARIANTS = {"pick": {}}
+    for v in sys.argv[3].split(";"):
+        name, spec = v.split(":")
+        VARIANTS[name] = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in spec.split(",")}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 eng = enc.engine()
