@@ -56,16 +56,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(pattern: str, profile: str):
-    """HBM bytes per launch of the kernels matching ``pattern`` (dispatch-weighted average) from a
-    committed rocprofv3 PMC summary (tools/pmc_traffic.sh -> profiles/*.json), or None."""
+# committed PMC passes (tools/pmc_all.sh) per (mode, GEMM rows per launch)
+PMC_PROFILES = {("w4a16", 16384): "r1_pmc_traffic_w4a16.json", ("w4a16", 8192): "r2_pmc_traffic_w4a16_m8192.json",
+                ("w4a8", 16384): "r2_pmc_traffic_w4a8_m16384.json", ("w8a8", 4096): "r2_pmc_traffic_w8a8_m4096.json"}
+
+
+def pmc_traffic(mode: str, profile: str):
+    """HBM bytes per launch of the mode's projection GEMMs (``is_proj_gemm``; dispatch-weighted
+    average) from a committed rocprofv3 PMC summary (tools/pmc_all.sh -> profiles/*.json), or None."""
     f = REPO / "profiles" / profile
     if not f.exists():
         return None, None
     d = json.loads(f.read_text())
     tot = n = 0
     for k, v in d["kernels"].items():
-        if pattern in k and v.get("hbm_bytes_avg"):
+        if is_proj_gemm(mode, k) and v.get("hbm_bytes_avg"):
             tot += v["hbm_bytes_avg"] * v["dispatches"]
             n += v["dispatches"]
     return (round(tot / n) if n else None), f"profiles/{profile}: " + d["source"]
@@ -103,8 +108,8 @@ def gemm_roofline(eng, bufs_batch: int, reps: int = 3):
         for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
             alg.append(rows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + rows * lin.outfeatures * out_b)
     # committed PMC passes per GEMM row count: M = 16384 (one B=4 chain), M = 8192 (a 2-image lane)
-    prof = {16384: "r1_pmc_traffic_w4a16.json", 8192: "r1_pmc_traffic_w4a16_m8192.json"}.get(rows)
-    traffic, src = pmc_traffic("w4a16_gemm", prof) if prof else (None, None)
+    prof = PMC_PROFILES.get(("w4a16", rows))
+    traffic, src = pmc_traffic("w4a16", prof) if prof else (None, None)
     return dict(bound="mfma", achieved=round(achieved, 1), peak=PEAK_FP16_TFLOPS, unit="TFLOP/s",
                 frac=round(achieved / PEAK_FP16_TFLOPS, 4), traffic=traffic,
                 traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
@@ -244,6 +249,13 @@ def w8a8_roofline(eng, batch: int):
                 frac=round(achieved / PEAK_INT8_TOPS, 4), traffic=None,
                 kernel="i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)", launches_timed=n,
                 avg_launch_us=round(t / n * 1e6, 2))
+
+
+def gemm_shapes(mode, eng):
+    """Per block: the (K, N) of qkv, proj, lin1, lin2."""
+    if mode == "w8a8":
+        return [tuple((bl[k]["k"], bl[k]["n"]) for k in ("qkv", "proj", "lin1", "lin2")) for bl in eng.blocks]
+    return [tuple((lin.infeatures, lin.outfeatures) for lin in (p.qkv, p.proj, p.lin1, p.lin2)) for p in eng.plans]
 
 
 def gemm_flops_per_step(mode, eng, images):
@@ -510,20 +522,22 @@ def main():
     skip = args.no_isolated
     iso = (dict(achieved=None, frac=None, avg_launch_us=None, launches_timed=0) if skip else
            {"w4a16": gemm_roofline, "w4a8": w4a8_roofline, "w8a8": w8a8_roofline}[mode](eng, per_launch_imgs))
-    if mode == "w4a16":
-        alg = []
-        trows = per_launch_imgs * 4096
-        for p in eng.plans:
-            for lin, out_b in ((p.qkv, 2), (p.proj, 8), (p.lin1, 2), (p.lin2, 8)):
-                alg.append(trows * lin.infeatures * 2 + lin.infeatures * lin.outfeatures // 2 + trows * lin.outfeatures * out_b)
-        profile = {16384: "r1_pmc_traffic_w4a16.json", 8192: "r1_pmc_traffic_w4a16_m8192.json"}.get(trows)
-        traffic, src = pmc_traffic("w4a16_gemm", profile) if profile else (None, None)
-        kernel = "w4a16_gemm_pp2 (qkv, lin1) + w4a16_gemm_v3 (proj, lin2): all 4 ViT-H projection shapes"
-        alg_b = round(sum(alg) / len(alg))
-    else:
-        traffic, src, alg_b = None, None, None
-        kernel = ("i8_gemm_pp2 / i8_gemm_kernel W4 (int4 x int8 MFMA, all 4 ViT-H projection shapes)" if mode == "w4a8"
-                  else "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes + neck 1x1)")
+    # algorithmic bytes per GEMM launch: A once, packed W once, the output (fp32 residual = read +
+    # write) once -- per mode: (A bytes/elem, W bytes/elem, out bytes/elem per layer)
+    trows = per_launch_imgs * (eng.enc.img_size // eng.patch) ** 2 if mode == "w8a8" else per_launch_imgs * 4096
+    a_b, w_b, outs = {"w4a16": (2, 0.5, (2, 8, 2, 8)), "w4a8": (1, 0.5, (2, 8, 1, 8)),
+                      "w8a8": (1, 1, (1, 2, 1, 2))}[mode]
+    alg = []
+    for kn in gemm_shapes(mode, eng):
+        for (k, n), out_b in zip(kn, outs):
+            alg.append(trows * k * a_b + k * n * w_b + trows * n * out_b)
+    alg_b = round(sum(alg) / len(alg))
+    profile = PMC_PROFILES.get((mode, trows))
+    traffic, src = pmc_traffic(mode, profile) if profile else (None, None)
+    kernel = {"w4a16": "w4a16_gemm_pp2 (32x32x16 MFMA for qkv / lin1, 16x16x32 for proj / lin2): all 4 ViT-H "
+                       "projection shapes",
+              "w4a8": "i8_gemm_pp2 (int4 x int8 MFMA, zero point through row sums): all 4 ViT-H projection shapes",
+              "w8a8": "i8_gemm_kernel W8 (int8 x int8 MFMA, vit_b projection shapes)"}[mode]
     flops_step = gemm_flops_per_step(mode, eng, rows)
     live = dict(achieved=iso["achieved"], frac=iso["frac"], avg_launch_us=iso["avg_launch_us"],
                 launches_timed=iso["launches_timed"],

@@ -870,6 +870,26 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
 // phase 0.  STAGES-slot ring: K tile kt+STAGES-1 is staged during tile kt (phases 1..NPH-1).
 __device__ unsigned long long g_pp_stamps[8];   // timing experiments only (cfg 73)
 
+// Tile of workgroup bid.  Default (xcd_remap): XCD x owns the x-th contiguous eighth of the
+// row-major tile order, i.e. whole M-rows of tiles across ALL N tiles, so every XCD streams the
+// whole packed weight (3.3 MB for lin1) through its 4 MB L2 once per round of 32 tiles -- the
+// output stream evicts it in between (PMC: lin1 fetches 4.3x its algorithmic bytes).
+// blocked2d (tiles_n even, tiles_m % 4 == 0, nwg % 8 == 0): XCD x owns the rectangle of M-rows
+// [(x>>1) tm/4, +tm/4) x N-tiles [(x&1) tn/2, +tn/2): half of the weight per XCD stays resident
+// while each A panel is read by the tn/2 concurrent tiles of its row.
+__device__ __forceinline__ void xcd_tile(int bid, int tiles_m, int tiles_n, bool blocked2d, int& mt, int& nt) {
+  const int nwg = tiles_m * tiles_n;
+  if (blocked2d && (tiles_n & 1) == 0 && (tiles_m & 3) == 0) {
+    const int x = bid & 7, k = bid >> 3, bm = tiles_m >> 2, bn = tiles_n >> 1;
+    mt = (x >> 1) * bm + k / bn;
+    nt = (x & 1) * bn + k % bn;
+    return;
+  }
+  const int t = xcd_remap(bid, nwg);
+  mt = t / tiles_n;
+  nt = t % tiles_n;
+}
+
 __host__ __device__ constexpr int pp2_pre(int p, int npw, int nph, int first) {   // pieces before phase p
   return p <= first ? 0 : (npw * (p - first)) / (nph - first);
 }
@@ -935,9 +955,10 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   const int grp = wave >> 2;
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int m0 = (bid / tiles_n) * BM;
-  const int n0 = (bid % tiles_n) * BN;
+  int m0, n0;
+  xcd_tile(blockIdx.x, tiles_m, tiles_n, (VAR & 64) != 0, m0, n0);
+  m0 *= BM;
+  n0 *= BN;
   const int kt_count = K / BK;
 
   const char* src[NPW];
@@ -1242,6 +1263,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // (measured: 57 -> 66 +1-3 %, 64 -> 67 within +-2 %, in-graph no change; DESIGN dead ends)
       case 66: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 32>(a, st);
       case 67: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 48>(a, st);
+      // 2-D XCD tile blocks (xcd_tile): lin1 PMC fetch 105.7 -> 92.3 MB per M = 8192 launch,
+      // time unchanged isolated (121.3 vs 122.0 us) and in the graph (23.98 / 23.94 vs 23.99 ms)
+      case 68: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 64>(a, st);
+      case 69: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 80>(a, st);
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1331,7 +1356,7 @@ static int cfg_bn(int cfg) {
                  case 31: return 320; case 32: return 256; case 33: return 256; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
                  case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
-                 case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 66: return 256; case 67: return 256;
+                 case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 68: return 256; case 69: return 256; case 66: return 256; case 67: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }
 }
