@@ -62,6 +62,27 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return fmaf(-ax, poly * e, fmaxf(x, 0.0f));
 }
 
+typedef float float2_t __attribute__((ext_vector_type(2)));
+
+// gelu_fast on two values with packed fp32 math (v_pk_fma_f32 / v_pk_mul_f32 carry two values per
+// instruction: twice the VALU rate in an epilogue, where no MFMA shares the issue): the same IEEE
+// operations in the same order as gelu_fast, so each half is bit-identical to it
+__device__ __forceinline__ float2_t gelu_fast2(float2_t x) {
+  const float2_t ax = __builtin_elementwise_abs(x);
+  const float2_t d = __builtin_elementwise_fma((float2_t)(0.2316418883f), ax, (float2_t)(1.0f));
+  const float2_t t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  float2_t poly = __builtin_elementwise_fma((float2_t)(0.5307027145f), t, (float2_t)(-0.7265760135f));
+  poly = __builtin_elementwise_fma(poly, t, (float2_t)(0.7107068705f));
+  poly = __builtin_elementwise_fma(poly, t, (float2_t)(-0.142248368f));
+  poly = __builtin_elementwise_fma(poly, t, (float2_t)(0.127414796f));
+  poly = poly * t;
+  const float2_t u = ax * (float2_t)(0.84932180028801904272f);
+  const float2_t nu2 = -(u * u);
+  const float2_t e = {__builtin_amdgcn_exp2f(nu2.x), __builtin_amdgcn_exp2f(nu2.y)};
+  const float2_t m = {fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)};
+  return __builtin_elementwise_fma(-ax, poly * e, m);
+}
+
 // clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
 // quantizer/uniform.py:31-36), at the price of a multiply: q = v * inv (inv = fl(1/s)) is within
 // ~1.2e-7 |q| of v / s and fl(v / s) within 6e-8 |q|, so rint(q) == rint(fl(v / s)) unless q lies

@@ -97,15 +97,19 @@ __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], cons
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 16; r += 2) {   // accumulator pairs (r, r + 1) = slice rows (rl, rl + 1): packed fp32
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        int a = acc[i][t][r];
-        if constexpr (ZPS) a -= zpv[t] * ssum[i * 32 + rl];
-        float v = (float)a * csc[t] + cb[t];
-        if (GELU) v = gelu_fast(v);
-        ep[rl * WN + t * 32 + (lane & 31)] = v;
+        int a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
+        if constexpr (ZPS) {
+          a0 -= zpv[t] * ssum[i * 32 + rl];
+          a1 -= zpv[t] * ssum[i * 32 + rl + 1];
+        }
+        float2_t v = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]), (float2_t)(cb[t]));
+        if (GELU) v = gelu_fast2(v);
+        ep[rl * WN + t * 32 + (lane & 31)] = v.x;
+        ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);

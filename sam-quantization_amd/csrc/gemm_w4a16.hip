@@ -811,14 +811,16 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
 #pragma unroll
     for (int sl = 0; sl < NSL; ++sl) {
 #pragma unroll
-      for (int rq = 0; rq < 16 / NSL; ++rq) {
+      for (int rq = 0; rq < 16 / NSL; rq += 2) {   // accumulator pairs (r, r + 1): packed fp32 math
         const int r = sl * (16 / NSL) + rq;
-        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel - sl * EP_ROWS;   // row within the slice
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel - sl * EP_ROWS;   // row within the slice (r + 1: rl + 1)
 #pragma unroll
         for (int t = 0; t < TN; ++t) {
-          float v = acc[i][t][r] * csc[t] + cb[t];
-          if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast(v);
-          ep[rl * WN + t * 32 + (lane & 31)] = v;
+          float2_t v = __builtin_elementwise_fma((float2_t){acc[i][t][r], acc[i][t][r + 1]}, (float2_t)(csc[t]),
+                                                 (float2_t)(cb[t]));
+          if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast2(v);
+          ep[rl * WN + t * 32 + (lane & 31)] = v.x;
+          ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
