@@ -864,6 +864,31 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
 }
 
 
+// Direct epilogue of a TRANSPOSED accumulator (VAR & 128: the MFMA is issued as W^T . A^T, so a
+// lane's accumulator registers run along N): every lane holds G consecutive output columns of ONE
+// row per register group and stores them straight from registers (G = 4: 8 bytes of fp16 or 16
+// bytes of fp32, a 16-byte read-modify-write for the residual) -- no LDS staging round trip
+// (ds_write_b32 per element + ds_read_b128 + waits in pp_epilogue).  v[q] = acc[q] * s[n] + b[n].
+template <int EPI>
+__device__ __forceinline__ void te_store4(const float4_t& acc, const float4_t& sc, const float4_t& bi, void* Cout,
+                                          int64_t ldc, int M, int row, int col) {
+  if (row >= M) return;
+  float2_t v0 = __builtin_elementwise_fma((float2_t){acc[0], acc[1]}, (float2_t){sc[0], sc[1]}, (float2_t){bi[0], bi[1]});
+  float2_t v1 = __builtin_elementwise_fma((float2_t){acc[2], acc[3]}, (float2_t){sc[2], sc[3]}, (float2_t){bi[2], bi[3]});
+  if (EPI == SAMQ_EPI_BIAS_GELU) {
+    v0 = gelu_fast2(v0);
+    v1 = gelu_fast2(v1);
+  }
+  if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+    float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col);
+    const float4_t v = {v0.x, v0.y, v1.x, v1.y};
+    if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+  } else {
+    const half2_t h0 = __builtin_convertvector(v0, half2_t), h1 = __builtin_convertvector(v1, half2_t);
+    *(half4_t*)((_Float16*)Cout + (int64_t)row * ldc + col) = half4_t{h0.x, h0.y, h1.x, h1.y};
+  }
+}
+
 // ------------------------------------------------------------------ GEMM v6 (ping-pong, k-phases)
 // As v5, but a phase is a K-PART of the tile over ALL of the wave's output tiles: phase p
 // multiplies k16-steps [p*KPP, (p+1)*KPP) for TM x TN accumulators, so every phase reads its own
@@ -937,6 +962,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // VAR & 16: v_mfma_f32_16x16x32_f16 fragments (same tile, LDS bytes and unpack count; the chip
   // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
   constexpr bool M16 = (VAR & 16) != 0;
+  constexpr bool TE = (VAR & 128) != 0;   // transposed accumulators + direct epilogue (te_store4)
   constexpr int KS32 = 2 / NPH;                  // M16: k32 steps per phase
   constexpr int EP_ROWS = WN > 64 ? 16 : 32;
   constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : EP_ROWS * WN * 4;
@@ -1141,7 +1167,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
             for (int t = 0; t < TN; ++t)
 #pragma unroll
               for (int h = 0; h < 2; ++h)
-                acc16[i][t][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af16[i][s], bf16[t][h][s], acc16[i][t][h], 0, 0, 0);
+                acc16[i][t][h] = TE ? __builtin_amdgcn_mfma_f32_16x16x32_f16(bf16[t][h][s], af16[i][s], acc16[i][t][h], 0, 0, 0)
+                                    : __builtin_amdgcn_mfma_f32_16x16x32_f16(af16[i][s], bf16[t][h][s], acc16[i][t][h], 0, 0, 0);
       } else {
 #pragma unroll
         for (int s = 0; s < KPP; ++s)
@@ -1152,7 +1179,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
               if (VAR & 2) {   // timing-only: no MFMA
                 acc[i][t][0] += (float)af[i][s][0] * (float)bf[t][s][1];
               } else {
-                acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+                acc[i][t] = TE ? __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[t][s], af[i][s], acc[i][t], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
               }
             }
       }
@@ -1175,6 +1203,42 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     atomicAdd(&g_pp_stamps[4], (unsigned long long)kt_count * NPH);
   }
 
+  if constexpr (M16 && TE) {
+    // lane (ql, g16) holds row 16 i + ql, columns 32 t + 16 h + 4 g16 .. +3 of the wave's tile
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = n0 + wn * WN + 32 * t + 16 * h + 4 * g16;
+        const half4_t s4 = *(const half4_t*)(scales + c);
+        const half4_t b4 = bias ? *(const half4_t*)(bias + c) : half4_t{0, 0, 0, 0};
+        const float4_t sc = {(float)s4[0], (float)s4[1], (float)s4[2], (float)s4[3]};
+        const float4_t bi = {(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
+#pragma unroll
+        for (int i = 0; i < 2 * TM; ++i)
+          te_store4<EPI>(acc16[i][t][h], sc, bi, Cout, ldc, M, m0 + wm * WM + 16 * i + ql, c);
+      }
+    return;
+  }
+  if constexpr (!M16 && TE) {
+    // lane (l32, hsel) holds row 32 i + l32, columns 32 t + 8 j + 4 hsel .. +3 in register group j
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = n0 + wn * WN + 32 * t + 8 * j + 4 * hsel;
+        const half4_t s4 = *(const half4_t*)(scales + c);
+        const half4_t b4 = bias ? *(const half4_t*)(bias + c) : half4_t{0, 0, 0, 0};
+        const float4_t sc = {(float)s4[0], (float)s4[1], (float)s4[2], (float)s4[3]};
+        const float4_t bi = {(float)b4[0], (float)b4[1], (float)b4[2], (float)b4[3]};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float4_t a = {acc[i][t][4 * j], acc[i][t][4 * j + 1], acc[i][t][4 * j + 2], acc[i][t][4 * j + 3]};
+          te_store4<EPI>(a, sc, bi, Cout, ldc, M, m0 + wm * WM + 32 * i + (lane & 31), c);
+        }
+      }
+    return;
+  }
   if constexpr (M16) {
     float csc16[TN][2], cb16[TN][2];
 #pragma unroll
@@ -1269,6 +1333,11 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // time unchanged isolated (121.3 vs 122.0 us) and in the graph (23.98 / 23.94 vs 23.99 ms)
       case 68: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 64>(a, st);
       case 69: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 80>(a, st);
+      // transposed accumulators (W^T . A^T) stored straight from registers (te_store4), no LDS
+      // staging: bit-identical, but qkv 73.5 -> 113.1 us (52) / 72.7 -> 85.9 us (53) at M = 8192 --
+      // the row-scattered 8-byte stores are issue-bound; only the fp32 residual on 16x16 ties
+      case 52: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 128>(a, st);
+      case 53: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 144>(a, st);
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1357,7 +1426,7 @@ static int cfg_bn(int cfg) {
                  case 27: return 256; case 28: return 256; case 29: return 320; case 30: return 320;
                  case 31: return 320; case 32: return 256; case 33: return 256; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
-                 case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
+                 case 52: return 256; case 53: return 256; case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
                  case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 68: return 256; case 69: return 256; case 66: return 256; case 67: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }

@@ -1,5 +1,5 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 400 python -m pytest tests/test_w8a8.py -q -x -m gpu > gpurun_out/g11_tests.log 2>&1 || exit $?
-BENCH_ARGS="--mode w8a8 --steps 40 --warmup 5" timeout -k 10 600 bash tools/bench_variants.sh build_ab/old_q8.so build_ab/new.so > gpurun_out/g11_var88.log 2>&1 || exit $?
-BENCH_ARGS="--mode w8a8 --steps 40 --warmup 5" timeout -k 10 600 bash tools/bench_variants.sh build_ab/old_q8.so build_ab/new.so >> gpurun_out/g11_var88.log 2>&1
+timeout -k 10 240 python tools/bench_gemm.py --m 8192 --cfgs 57,52,64,53 --iters 20 > gpurun_out/g12_m8192.log 2>&1 || exit $?
+timeout -k 10 300 python tools/bench_gemm.py --m 65536 --cfgs 57,52,64,53 --iters 5 > gpurun_out/g12_m65536.log 2>&1 || exit $?
+timeout -k 10 400 python tools/bench_cfg_ab.py 2 8 "te_all:qkv=52,lin1=52,proj=53,lin2=53;te_wide:qkv=52,lin1=52;te_narrow:proj=53,lin2=53" > gpurun_out/g12_ab.log 2>&1
