@@ -1075,6 +1075,9 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       }
   }
 
+  // VAR & 256: static priority instead of per-segment flips -- the second-dispatched half (group 1,
+  // the arbitration loser) at prio 1 for the whole loop (MI355X_MICROARCH.md two-waves item 4)
+  if ((VAR & 256) && grp) __builtin_amdgcn_s_setprio(1);
   // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
   const int pro = kt_count < LA ? kt_count : LA;
 #pragma unroll
@@ -1157,7 +1160,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       __builtin_amdgcn_sched_barrier(0);
       if (VAR & 4) stamp(1);
       // ---------------- MFMA half
-      __builtin_amdgcn_s_setprio(1);
+      if (!(VAR & 256)) __builtin_amdgcn_s_setprio(1);
       if constexpr (M16) {
 #pragma unroll
         for (int s = 0; s < KS32; ++s)
@@ -1188,7 +1191,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       // the barrier otherwise; WAR-safe in every phase: see header)
       if (pf && !DMA_LOAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
       if (VAR & 4) stamp(2);
-      __builtin_amdgcn_s_setprio(0);
+      if (!(VAR & 256)) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
@@ -1338,6 +1341,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // the row-scattered 8-byte stores are issue-bound; only the fp32 residual on 16x16 ties
       case 52: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 128>(a, st);
       case 53: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 144>(a, st);
+      // static priority (group 1 at prio 1 for the whole loop, no per-segment flips): isolated
+      // within +-2 %, in the 2-lane graph 24.41 (all 59) vs 24.39 (all 64) vs 24.48 ms (pick)
+      case 54: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 256>(a, st);
+      case 59: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 272>(a, st);
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1426,7 +1433,7 @@ static int cfg_bn(int cfg) {
                  case 27: return 256; case 28: return 256; case 29: return 320; case 30: return 320;
                  case 31: return 320; case 32: return 256; case 33: return 256; case 41: return 256; case 42: return 256;
                  case 43: return 128; case 44: return 64; case 45: return 256;
-                 case 52: return 256; case 53: return 256; case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
+                 case 52: return 256; case 53: return 256; case 54: return 256; case 59: return 256; case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
                  case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 68: return 256; case 69: return 256; case 66: return 256; case 67: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
                  default: return 0; }
