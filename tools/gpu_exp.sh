@@ -1,8 +1,4 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py tests/test_w4a8.py -q -x -m gpu -k "patch or conv or embed or neck" > gpurun_out/g18_tests.log 2>&1 || exit $?
-for lib in old_conv new; do
-  for mode in w4a8 w4a16; do
-    SAMQ_LIB=$PWD/sam-quantization_amd/build_ab/$lib.so timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/g18_${lib}_$mode -o run --output-format csv -- python3 bench.py --mode $mode --steps 5 --warmup 2 --no-cpu-baseline --no-isolated > gpurun_out/g18_${lib}_$mode.log 2>&1 || exit $?
-  done
-done
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/g19_pmc -o p1 -- python3 tools/bench_gemm.py --m 65536 --cfgs 57,64 --shapes qkv,lin1,lin2,proj --iters 2 > gpurun_out/g19_pmc.log 2>&1 || exit 1
+timeout -k 10 200 python3 tools/bench_gemm.py --m 65536 --cfgs 57,64 --shapes qkv,lin1,lin2,proj --iters 5 > gpurun_out/g19_time.log 2>&1
