@@ -48,25 +48,56 @@ class W4A8EncoderOracle(EncoderOracle):
         return x
 
     def block(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        return self.block_taps(i, x)["out"]
+
+    def block_taps(self, i: int, x: torch.Tensor) -> dict:
+        """One block with every intermediate recorded (the stage-local parity taps): ``ln1`` /
+        ``ln2`` the LayerNorm outputs (natural token layout, before the int8 quantiser), ``qkv``
+        the qkv projection and ``att`` the attention output (natural layout: window padding
+        cropped), ``x1`` the residual after proj, ``h`` GELU(lin1), ``out`` the block output."""
         cfg, p = self.cfg, self.p
         pre = f"blocks.{i}."
         c = cfg["embed_dim"]
         win = 0 if i in cfg["global_attn_indexes"] else cfg["window_size"]
-        shortcut = x
+        t = {"x": x}
         y = F.layer_norm(x, (c,), p[pre + "norm1.weight"], p[pre + "norm1.bias"], eps=1e-6)
+        t["ln1"] = y
         h, w = y.shape[1], y.shape[2]
         if win > 0:
             y, pad_hw = window_partition(y, win)
         qkv = F.linear(self.qin(pre + "attn.qkv", y), p[pre + "attn.qkv.weight"], p.get(pre + "attn.qkv.bias"))
         o = attention_core(qkv, cfg["num_heads"], p[pre + "attn.rel_pos_h"], p[pre + "attn.rel_pos_w"])
+        t["qkv"] = window_unpartition(qkv, win, pad_hw, (h, w)) if win > 0 else qkv
+        t["att"] = window_unpartition(o, win, pad_hw, (h, w)) if win > 0 else o
         y = F.linear(self.qin(pre + "attn.proj", o), p[pre + "attn.proj.weight"], p.get(pre + "attn.proj.bias"))
         if win > 0:
             y = window_unpartition(y, win, pad_hw, (h, w))
-        x = shortcut + y
+        x = x + y
+        t["x1"] = x
         z = F.layer_norm(x, (c,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], eps=1e-6)
+        t["ln2"] = z
         z = F.gelu(F.linear(self.qin(pre + "mlp.lin1", z), p[pre + "mlp.lin1.weight"], p.get(pre + "mlp.lin1.bias")))
+        t["h"] = z
         z = F.linear(self.qin(pre + "mlp.lin2", z), p[pre + "mlp.lin2.weight"], p.get(pre + "mlp.lin2.bias"))
-        return x + z
+        t["out"] = x + z
+        return t
+
+    def attention(self, i: int, qkv: torch.Tensor) -> torch.Tensor:
+        """The block-``i`` attention core on a natural-layout qkv (windowed blocks partition it
+        with the pad tokens' q/k/v = the qkv bias, which is what the zero-padded LN output
+        projects to), cropped back to the natural layout."""
+        cfg, p = self.cfg, self.p
+        pre = f"blocks.{i}."
+        win = 0 if i in cfg["global_attn_indexes"] else cfg["window_size"]
+        h, w = qkv.shape[1], qkv.shape[2]
+        if win > 0:
+            bias = p.get(pre + "attn.qkv.bias")
+            real, _ = window_partition(torch.ones_like(qkv[..., :1]), win)
+            qkv, pad_hw = window_partition(qkv, win)
+            if bias is not None:
+                qkv = torch.where(real > 0, qkv, bias.to(qkv.dtype))
+        o = attention_core(qkv, cfg["num_heads"], p[pre + "attn.rel_pos_h"], p[pre + "attn.rel_pos_w"])
+        return window_unpartition(o, win, pad_hw, (h, w)) if win > 0 else o
 
     @torch.no_grad()
     def calibrate(self, images) -> None:

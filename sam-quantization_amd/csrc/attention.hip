@@ -138,7 +138,9 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
   // (image, head) all land on one XCD (workgroups are dealt round-robin over the 8 XCDs), so that
   // XCD's L2 serves their shared K/V stream instead of every XCD fetching every head's keys
   int qblk = blockIdx.x, head = blockIdx.y, unit = blockIdx.z;
-  if (!RESIDENT && gridDim.y == 1 && gridDim.z == 1) {
+  // p.nqb > 0 only on the 1-D launch (launch_attn sets it there); a 3-D launch whose y / z
+  // extents happen to be 1 (heads * units == 1) keeps blockIdx as is
+  if (!RESIDENT && p.nqb > 0) {
     const int nqb = p.nqb, pairs = p.heads * p.units;
     const int xcd = blockIdx.x & 7, k = blockIdx.x >> 3;
     const int pair = xcd * (pairs >> 3) + k / nqb;

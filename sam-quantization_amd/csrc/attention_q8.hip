@@ -348,8 +348,12 @@ __device__ __forceinline__ void q8_rel_block(const AttnQ8Params& p, const int8_t
 // chunk's global loads in flight under the current chunk's math.  Per chunk and wave:
 //   S^T = K.Q^T on 4 x v_mfma_i32_16x16x64_i8 (exact int32; lane = query ql, keys 16bb+4g+i);
 //   c = q8(q8(st * s_qkv^2 * scale, s_a1) * s_a1 + rel_h[kh] + rel_w[kw], s_a2): the two score
-//       quantisers (reciprocal multiply, round-half-even, clamp) in the reference's addition order
-//       (fq_vit image_encoder.py:455-470; rel_w indexed by the query ROW, quirk 1);
+//       quantisers (reciprocal multiply, round-half-even, clamp) of fq_vit image_encoder.py:455-470
+//       (rel_w indexed by the query ROW, quirk 1).  NOT bit-exact: the second argument is
+//       evaluated as fma(code1, s_a1/s_a2, (rel_h + rel_w)/s_a2) -- pre-scaled terms in another
+//       addition order than the reference's (code1*s_a1 + rel_h + rel_w)/s_a2 -- so a code can move
+//       by one at a .5 tie; test_w8a8_stage_local_parity bounds that (all codes within +-1, at
+//       most 1e-4 of them off by one);
 //   online softmax on the integer codes, p = exp2(c * k2 - m * k2) (one fma + exp2);
 //   O^T += V^T.P^T on 16x16x32 f16 MFMAs with P split hi + lo (|P - hi - lo| ~ 2^-22 |P|), V^T
 //       fragments by ds_read_b64_tr_b16 from the row-major fp16 V; the softmax denominators come

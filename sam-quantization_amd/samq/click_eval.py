@@ -55,28 +55,44 @@ def get_next_click_torch(prev_seg: torch.Tensor, gt_semantic_seg: torch.Tensor,
 
 @torch.no_grad()
 def click_iou(prompt_encoder, mask_decoder, image_embedding: torch.Tensor, gt_masks: torch.Tensor,
-              num_clicks: int = 5, seed: int = 0, ignore_label: int = -1) -> List[float]:
+              num_clicks: int = 5, seed: int = 0, ignore_label: int = -1, clicks=None,
+              return_trace: bool = False):
     """The reference's click loop for ONE image embedding ``(1, 256, 64, 64)`` and ``gt_masks``
     ``(B, 1, H, W)`` (B objects of that image, each its own episode).  Returns the IoU after every
-    click for each object: ``[[iou_click1, ..., iou_clickN], ...]``."""
+    click for each object: ``[[iou_click1, ..., iou_clickN], ...]``.
+
+    ``clicks`` (from an earlier call's trace) replays that click sequence instead of sampling it:
+    the same (point, label) prompts with this embedding's own low-res logits fed back, so two
+    encoders can be compared mask by mask along one episode.  ``return_trace=True`` returns
+    ``(ious, trace)`` with ``trace[b] = {"clicks": [(xy, label), ...], "masks": [bool (H, W), ...]}``."""
     dev = image_embedding.device
     rng = np.random.Generator(np.random.PCG64(seed))
-    out = []
+    out, trace = [], []
     for b in range(gt_masks.shape[0]):
         gt = gt_masks[b:b + 1].to(dev)
         prev = torch.zeros_like(gt, dtype=torch.float32)
         pts, lbls, low, ious = [], [], None, []
+        tr = {"clicks": [], "masks": []}
         for k in range(num_clicks):
-            p, lab = get_next_click_torch(prev, gt, rng)
-            pts.append(torch.cat(p).to(dev).float())
-            lbls.append(torch.cat(lab).to(dev))
+            if clicks is None:
+                p, lab = get_next_click_torch(prev, gt, rng)
+                p, lab = torch.cat(p), torch.cat(lab)
+            else:
+                xy, lv = clicks[b]["clicks"][k]
+                p, lab = torch.tensor([[xy]]), torch.tensor([[lv]])
+            tr["clicks"].append(((int(p[0, 0, 0]), int(p[0, 0, 1])), int(lab[0, 0])))
+            pts.append(p.to(dev).float())
+            lbls.append(lab.to(dev))
             sparse, dense = prompt_encoder(points=(torch.cat(pts, 1), torch.cat(lbls, 1)), boxes=None,
                                            masks=None if k == 0 else low)
             low, _ = mask_decoder(image_embedding.float(), prompt_encoder.get_dense_pe(), sparse, dense, False)
             prev = F.interpolate(low, size=gt.shape[-2:], mode="bilinear", align_corners=False)
             ious.append(float(get_iou(gt, prev > 0, ignore_label)))
+            if return_trace:
+                tr["masks"].append((prev > 0)[0, 0].cpu())
         out.append(ious)
-    return out
+        trace.append(tr)
+    return (out, trace) if return_trace else out
 
 
 def synthetic_gt_masks(n: int, size: int = 1024, seed: int = 0, ignore_band: int = 6) -> torch.Tensor:

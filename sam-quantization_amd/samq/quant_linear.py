@@ -21,7 +21,7 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 
 
 def make_quant(model: nn.Module, bits: int, groupsize: int) -> None:
@@ -72,7 +72,9 @@ class QuantLinear(nn.Module):
     @gemm_cfg.setter
     def gemm_cfg(self, cfg: int) -> None:
         cfg = int(cfg)
-        if cfg != 0 and cfg not in ops.W4A16_CFGS:
+        # the tuning build (SAMQ_LIB=tuning) also carries the timing-only / experimental configs;
+        # its C ABI range-checks them itself (SAMQ_ERR_INVALID for unknown ones)
+        if cfg != 0 and cfg not in ops.W4A16_CFGS and _lib.LIB_PATH.name != "libsamq_hip_tuning.so":
             raise ValueError(f"gemm_cfg {cfg} is not a product tile config (0 or one of {sorted(ops.W4A16_CFGS)})")
         self._gemm_cfg = cfg
 

@@ -352,7 +352,10 @@ class SamPredictor:
         self.original_size = tuple(original_image_size)
         self.input_size = tuple(transformed_image.shape[-2:])
         enc = self.model.image_encoder
-        if transformed_image.is_cuda and transformed_image.dtype == torch.uint8 and enc.is_quantized():
+        # only the GPTQ encoder (samq.modeling) has the uint8 patch-embedding entry; any other
+        # encoder (e.g. the fq_vit W8A8 one, which has no ``is_quantized``) takes preprocess + forward
+        fused_u8 = getattr(enc, "is_quantized", None)
+        if transformed_image.is_cuda and transformed_image.dtype == torch.uint8 and fused_u8 is not None and fused_u8():
             # HIP engine: Sam.preprocess (normalise + zero-pad) runs inside the patch embedding
             # kernel on the raw uint8 pixels (samq_patch_embed_u8)
             self.features = enc.engine()(transformed_image.contiguous(), out_dtype=torch.float32,

@@ -99,3 +99,34 @@ def test_lanes_bit_identical(cuda, vith32, lanes):
     assert gout.stride() == ref.stride()   # same channels-last layout from every lane count
     with pytest.raises(ValueError):
         eng(x4[:3], lanes=2)
+
+
+def test_config4_per_gpu_workload_b8_lanes4(cuda, vith32):
+    """BASELINE config 4's per-GPU workload (ViT-H W4A16, 64 images over 8 GPUs = 8 per GPU) as
+    bench.py runs it: B = 8 in 4 lanes of 2 images, eager and captured into one HIP graph.
+    Bit-identical to one chain (every GEMM at M = 8192 per lane, the same tile picks as B = 2);
+    image 0 (the golden image) within the north-star tolerance of oracle G1 and equal to its own
+    B = 1 run up to batch-size-dependent tile picks (< 1e-4)."""
+    cfg, st, names, q, enc, img, _ = vith32
+    eng = enc.engine()
+    x1 = torch.from_numpy(img).to(cuda)
+    gen = torch.Generator(device="cpu").manual_seed(8)
+    rest = torch.randn((7,) + tuple(x1.shape[1:]), generator=gen).to(cuda)
+    x8 = torch.cat([x1, rest])
+    ref = eng(x8, out_dtype=torch.float32)
+    out = eng(x8, out_dtype=torch.float32, lanes=4)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    static = x8.clone()
+    graph, gout = eng.capture(static, out_dtype=torch.float32, lanes=4)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gout, ref)
+    assert torch.isfinite(gout).all()
+    one = eng(x1, out_dtype=torch.float32)
+    assert (one[0] - ref[0]).abs().max().item() < 1e-4
+    torch.set_num_threads(16)
+    g1 = oracle_g1(cfg, st, names, q)(img).numpy()
+    err = _report("config-4 per-GPU workload (B=8, 4 lanes) image 0 vs oracle G1", gout[:1].cpu().numpy(), g1)
+    assert err <= TOL
+    eng.release()

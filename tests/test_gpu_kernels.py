@@ -223,6 +223,8 @@ def _attn_case(b, h, w, heads, d, window, seed):
     (1, 32, 32, 2, 64, 0),
     (3, 16, 16, 2, 80, 0),
     (2, 14, 14, 2, 80, 0),      # pre-partitioned window as a global 14x14 grid (QuantAttention module path)
+    (1, 64, 64, 1, 80, 0),      # heads * B == 1: the 3-D grid launch (no XCD remap)
+    (1, 32, 32, 1, 64, 0),
 ])
 def test_rel_attention(cuda, b, h, w, heads, d, window):
     from samq import ops
@@ -255,6 +257,21 @@ def test_rel_attention_q_out(cuda, b, h, w, heads, d, window):
     assert got.dtype == torch.int8 and torch.equal(got, want)
     codes = np.clip(np.rint(ref / np.float32(s)), -128, 127)
     assert np.abs(got.cpu().numpy().astype(np.int32) - codes).max() <= 1
+
+
+@pytest.mark.parametrize("s,d", [(64, 80), (32, 64)])
+def test_attention_relbias_single_head(cuda, s, d):
+    """fused_attention.forward (samq_attention_relbias) at B = 1, heads = 1: the streaming kernel's
+    3-D grid launch, whose y / z extents are 1 (regression: the XCD remap is keyed on the
+    launcher's flag, not on the grid shape)."""
+    from samq import fused_attention
+    qkv16, _, rph, rpw, ref = _attn_case(1, s, s, 1, d, 0, seed=s + d)
+    qkv = _dev(qkv16, cuda)
+    q = qkv.reshape(1, s * s, 3, 1, d).permute(2, 0, 3, 1, 4).reshape(3, 1, s, s, d)[0]
+    rel_h, rel_w = fused_attention.add_decomposed_rel_pos(q, _dev(rph, cuda), _dev(rpw, cuda), (s, s), (s, s))
+    o = fused_attention.forward(qkv, rel_h, rel_w, 1, d, d ** -0.5)
+    torch.cuda.synchronize()
+    _close(o.reshape(ref.shape), ref, 3e-3)
 
 
 @pytest.mark.parametrize("tag", ["win", "glob"])

@@ -66,8 +66,9 @@ def test_w4a8_vith_vs_oracle(cuda):
 
     The int8 activation quantisers make the output sensitive to arithmetic differences upstream
     of them: the engine keeps the W4A16 path's fp16 attention, so a few % of the proj-input codes
-    sit one step away from the fp32 oracle's (measured per op in tools/debug_w4a8.py; the int4
-    GEMMs themselves are exact, test_w8a8.py::test_w4a8_gemm_exact_integer).  Stated tolerance
+    sit one step away from the fp32 oracle's (measured per stage in
+    test_w4a8_stage_local_parity; the int4 GEMMs themselves are exact,
+    test_w8a8.py::test_w4a8_gemm_exact_integer).  Stated tolerance
     (statistical): the distance to the W4A8 oracle is at most 1.5x the size of the int8
     activation noise itself (oracle W4A8 vs oracle W4A16), in max-abs and in mean-abs."""
     import samq
@@ -146,9 +147,14 @@ def test_w4a8_lanes_bit_identical_b8(cuda):
 @pytest.mark.gpu
 def test_w4a8_vith32_vs_oracle(cuda):
     """Full 32-block ViT-H W4A8 engine vs the W4A8 oracle fed the engine's own calibrated scales.
-    Stated tolerances: (relative) distance to the oracle <= 1.5x the int8 activation noise (oracle
-    W4A8 vs oracle W4A16) in max-abs and mean-abs, and (absolute) mean-abs <= 2.5e-2 and
-    max-abs <= 0.6 on outputs of absmax ~5 (measured: see the printed line)."""
+
+    Every stage is pinned to the oracle's codes by test_w4a8_stage_local_parity; end to end the
+    int8 quantisers amplify the rare one-code flips of the fp16 attention store (the oracle's
+    attention is fp32) over 32 blocks.  Measured (round 2, profiles/r2_v7_gputests.log): max-abs
+    0.255, mean-abs 3.93e-2 vs the int8 activation noise (oracle W4A8 vs oracle W4A16) of 0.206 /
+    3.27e-2, i.e. 1.24x / 1.20x the noise, on outputs of absmax ~5.  Stated bounds: <= 1.5x the
+    noise in max-abs and mean-abs, and absolutely max-abs <= 0.35, mean-abs <= 5e-2 (about 1.3x
+    the measured values)."""
     import samq
     cfg, st, names, q, o, enc = _w4a8_product(32, 7, cuda)
     scales = {}
@@ -168,3 +174,109 @@ def test_w4a8_vith32_vs_oracle(cuda):
           f"max-abs {nmax:.3e} mean-abs {nmean:.3e} | ref absmax {np.abs(ref).max():.3f}")
     assert err <= 1.5 * nmax and mean <= 1.5 * nmean
     assert mean <= 5e-2 and err <= 0.35
+
+
+def _codes(v, s):
+    """fq_vit's quantiser on a float tensor: clamp(round(v / s), -128, 127) (uniform.py:23-45)."""
+    return torch.clamp(torch.round(v / torch.tensor(s, dtype=torch.float32)), -128, 127)
+
+
+def _codes_close(out, ref, max_frac, what):
+    d = (out.cpu().to(torch.int64) - ref.to(torch.int64)).abs()
+    frac = float((d > 0).double().mean())
+    print(f"  {what:<28s} codes off by one {frac:.2e} (max |d| {int(d.max())})")
+    assert int(d.max()) <= 1, f"{what}: code off by {int(d.max())}"
+    assert frac <= max_frac, f"{what}: {frac:.2e} of codes off by one (> {max_frac:.1e})"
+    return frac
+
+
+def _float_close(out, ref, rtol, atol_frac, what):
+    out = out.cpu().float()
+    d = (out - ref).abs()
+    amax = float(ref.abs().max())
+    bad = d > rtol * ref.abs() + atol_frac * amax
+    print(f"  {what:<28s} max-abs {float(d.max()):.3e} (absmax {amax:.3f}), out of bound {int(bad.sum())}")
+    assert not bool(bad.any()), f"{what}: {int(bad.sum())} values off, max-abs {float(d.max()):.3e}"
+
+
+# off-by-one budgets: the integer-exact stages (LN-q, lin1 + GELU-q) may only differ from the
+# oracle's fp32 graph at rounding ties of its own fp32 sums; the attention store quantises an
+# fp16-arithmetic attention (fp16 Q/K/V/P on the MFMA, fp32 softmax) against the oracle's fp32
+# attention, measured (ViT-H, 1024^2, round 3) at 3.7e-3 (window) / 5.3e-3 (global) of codes --
+# bound 8e-3; the integer-exact stages measured 1e-6 .. 4e-6
+W4A8_EXACT_FRAC = 1e-4
+W4A8_ATTN_FRAC = 8e-3
+
+
+@pytest.mark.gpu
+def test_w4a8_stage_local_parity(cuda):
+    """Each fused W4A8 stage, fed the W4A8 oracle's own inputs, reproduces the oracle's int8 codes
+    (every code within +-1) or its float output (fp16 / fp32 rounding): the fp32 patch embedding;
+    per block LN1 + quantiser; the qkv int4 x int8 GEMM + bias (fp16 out); the attention with its
+    quantised store; proj + fp32 residual; LN2 + quantiser; lin1 + GELU + quantiser; lin2 + fp32
+    residual.  ViT-H geometry at 1024^2, block 0 windowed (with the 64 -> 70 window padding),
+    block 1 global.  Kernel-level code parity, the W4A8 counterpart of
+    test_w8a8.py::test_w8a8_stage_local_parity; the reference halves are fq_vit QAct
+    (layers.py:203-242 / uniform.py:23-45) and the GPTQ W4 linear (quant_linear.py:292-343)."""
+    import samq
+    from samq import ops
+    cfg, st, names, q, o = _oracle(2, 7, global_idx=(1,))
+    enc = product_encoder(cfg, st, names, q, -1, cuda).half()
+    samq.make_act_quant(enc)
+    torch.set_num_threads(16)
+    o.calibrate([synth.make_images(1, 1024, seed=1)])
+    for n, m in enc.named_modules():
+        if isinstance(m, samq.QuantLinear):
+            m.act_quant.quant = True
+            m.act_quant.quantizer.scale = torch.tensor([float(o.scales[n.replace("qkv_proj", "qkv").replace(
+                "o_proj", "proj")])], device=cuda)
+    eng = enc.engine()
+    assert eng.w4a8
+    img = synth.make_images(1, 1024, seed=9)
+    print()
+    with torch.no_grad():
+        x = o.embed(torch.from_numpy(img).half().float())
+        x_mine = torch.empty(x.shape, dtype=torch.float32, device=cuda)
+        eng.embed(torch.from_numpy(img).to(cuda).half(), x_mine)
+        # the product embeds the fp16 image (the reference runs model.half()); the oracle the fp32
+        # image of the same fp16 values
+        _float_close(x_mine, x, 1e-4, 2e-5, "patch embed (fp32)")
+        frac = {}
+        for i, pl in enumerate(eng.plans):
+            t = o.block_taps(i, x)
+            pre = f"blocks.{i}."
+            s_qkv, s_proj, s_l1, s_l2 = (float(o.scales[pre + k]) for k in ("attn.qkv", "attn.proj", "mlp.lin1",
+                                                                              "mlp.lin2"))
+            assert (pl.s_qkv, pl.s_proj, pl.s_lin1, pl.s_lin2) == (s_qkv, s_proj, s_l1, s_l2)
+            dev = lambda v: v.to(cuda).contiguous()
+            i8 = lambda v: dev(v.to(torch.int8))
+            kind = f"window {pl.window}" if pl.window else "global"
+            # LN1 + quantiser
+            ln1 = ops.layernorm_q(dev(t["x"]), pl.ln1_w, pl.ln1_b, pl.ln1_eps, out_scale=s_qkv)
+            c_ln1 = _codes(t["ln1"], s_qkv)
+            frac[pre + "ln1"] = _codes_close(ln1, c_ln1, W4A8_EXACT_FRAC, f"{pre}LN1-q")
+            # qkv GEMM (int32-exact sums, fp16 store) on the oracle's codes
+            qkv = pl.qkv.forward_w4a8(i8(c_ln1), s_qkv, ops.EPI_BIAS)
+            _float_close(qkv, t["qkv"], 2.0 ** -10, 1e-5, f"{pre}qkv GEMM")
+            # attention + quantised store on the same fp16 qkv the oracle gets
+            q16 = t["qkv"].half()
+            att = ops.rel_attention(dev(q16), pl.qkv_bias, pl.relh, pl.relw, pl.heads, pl.window, pl.scale,
+                                    out_scale=s_proj)
+            frac[pre + "att"] = _codes_close(att, _codes(o.attention(i, q16.float()), s_proj), W4A8_ATTN_FRAC,
+                                             f"{pre}attention ({kind})")
+            # proj + fp32 residual on the oracle's codes
+            x1 = dev(t["x"].clone())
+            pl.proj.forward_w4a8(i8(_codes(t["att"], s_proj)), s_proj, ops.EPI_RESADD_F32, out=x1)
+            _float_close(x1, t["x1"], 1e-5, 2e-6, f"{pre}proj + residual")
+            # LN2 + quantiser
+            c_ln2 = _codes(t["ln2"], s_l1)
+            frac[pre + "ln2"] = _codes_close(ops.layernorm_q(dev(t["x1"]), pl.ln2_w, pl.ln2_b, pl.ln2_eps,
+                                                             out_scale=s_l1), c_ln2, W4A8_EXACT_FRAC, f"{pre}LN2-q")
+            # lin1 + GELU + quantiser
+            hid = pl.lin1.forward_w4a8(i8(c_ln2), s_l1, ops.EPI_Q8_GELU, out_scale=s_l2)
+            frac[pre + "lin1"] = _codes_close(hid, _codes(t["h"], s_l2), W4A8_EXACT_FRAC, f"{pre}lin1 + GELU-q")
+            # lin2 + fp32 residual
+            x2 = dev(t["x1"].clone())
+            pl.lin2.forward_w4a8(i8(_codes(t["h"], s_l2)), s_l2, ops.EPI_RESADD_F32, out=x2)
+            _float_close(x2, t["out"], 1e-5, 2e-6, f"{pre}lin2 + residual")
+            x = t["out"]
