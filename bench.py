@@ -161,11 +161,16 @@ def is_proj_gemm(mode, name):
     return args[5] == ("1" if mode == "w4a8" else "0") and args[7] == "0"
 
 
-def in_step_from_profile(mode, imgs_per_launch, lanes, flops_step, peak):
+def instep_name(mode, imgs_per_launch, lanes, groupsize=-1):
+    g = f"_g{groupsize}" if groupsize and groupsize > 0 else ""
+    return f"instep_{mode}{g}_b{imgs_per_launch}_l{lanes}_{source_hash()}"
+
+
+def in_step_from_profile(mode, imgs_per_launch, lanes, flops_step, peak, groupsize=-1):
     """GEMM roofline of the timed replays (concurrent lanes included) from the committed rocprof
     kernel trace, restricted to bench's roctx-marked timed window: GEMM FLOPs of the window /
     summed GEMM dispatch time (tools/instep_profile.sh writes the JSON)."""
-    name = f"instep_{mode}_b{imgs_per_launch}_l{lanes}_{source_hash()}.json"
+    name = instep_name(mode, imgs_per_launch, lanes, groupsize) + ".json"
     f = REPO / "profiles" / name
     if not f.exists() or not flops_step:
         return None
@@ -543,7 +548,8 @@ def main():
                 launches_timed=iso["launches_timed"],
                 method="HIP events on the launch stream around every GEMM launch of one forward at the lane's "
                        "size, back to back with no concurrent lane (3 reps)")
-    ins = in_step_from_profile(mode, per_launch_imgs, args.lanes, flops_step, peak)
+    ins = in_step_from_profile(mode, per_launch_imgs, args.lanes, flops_step, peak,
+                               args.groupsize if mode == "w4a16" else -1)
     head = ins if ins else live
     roof = dict(bound="mfma", achieved=head["achieved"], peak=peak, unit="TFLOP/s", frac=head["frac"],
                 traffic=traffic, traffic_unit="bytes per launch (L2->fabric, PMC)", traffic_source=src,
@@ -569,7 +575,8 @@ def main():
             }[mode] + f", {batch} x 1024x1024 images per GPU", "mode": mode,
                        "model": model, "global_batch": gb, "per_gpu_batch": batch,
                        "seq_len": 4096, "parallelism": f"image-parallel x{world} (weights RCCL-broadcast once)",
-                       "graph": not args.no_graph, "lanes": args.lanes},
+                       "graph": not args.no_graph, "lanes": args.lanes,
+                       "groupsize": args.groupsize if mode == "w4a16" else -1},
             "roofline": roof,
             "e2e": {"tflop_per_image": round(fl["total"] / 1e12, 4), "achieved_tflops_per_gpu": round(e2e_tflops, 1),
                     "frac_of_fp16_peak": round(e2e_tflops / PEAK_FP16_TFLOPS, 4),

@@ -328,6 +328,16 @@ __device__ __forceinline__ half8_t w4_unpack(uint32_t w, const W4Unpack& k, cons
   const half2_t h3 = __builtin_bit_cast(half2_t, (w8 & k.m1) | k.g1) - z.z64;
   return half8_t{h0[0], h0[1], h1[0], h1[1], h2[0], h2[1], h3[0], h3[1]};
 }
+// grouped weights: the exact integers (q - zp) times the group's fp16 scale, one rounding
+__device__ __forceinline__ half8_t scale8(half8_t v, half2_t s) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const half2_t h = half2_t{v[2 * i], v[2 * i + 1]} * s;
+    v[2 * i] = h[0];
+    v[2 * i + 1] = h[1];
+  }
+  return v;
+}
 
 // The same epilogue for 16x16x32 accumulators (VAR & 16 of the ping-pong kernel): lane (ql, g)
 // of 16-row tile i, 32-column block t, half h holds rows 16i + 4g + r of column 32t + 16h + ql;
@@ -935,16 +945,29 @@ __global__ __launch_bounds__(512, 1)
 void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
                     const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
                     const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
-                    int M, int N, int K) {
+                    int M, int N, int K, int kpg) {
   constexpr int NW = 8;
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = TM * 32, WN = TN * 32;
   constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   constexpr int BK = 64, ROWB = BK * 2;
   constexpr int A_BYTES = BM * ROWB;
-  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB;
+  // VAR & 512: grouped weights (groupsize = 64 kpg < K).  Every wave stages, with each K tile, one
+  // more LDS-DMA piece: the group row of ITS OWN WN columns -- WN fp16 scales (lanes 0 .. WN/8-1) and
+  // WN/8 packed zero words (the next WN/32 lanes; the rest idle), GPB bytes -- so the wave's own
+  // retire wait covers it (no barrier): it reads tile kt+1's row right after that wait in tile kt's
+  // last load half and converts it in tile kt+1's phase 0 (only where a new group starts).  The
+  // unpack scales the exact integers once in fp16, fp16((q - zp) * s) (the v3 kernels' semantics),
+  // and the epilogue's per-channel scale is 1.
+  constexpr bool GR = (VAR & 512) != 0;
+  // timing-only (tuning build): VAR & 1024 skips the fp16 group scaling, VAR & 2048 the group row
+  constexpr bool G_NOSCALE = (VAR & 1024) != 0, G_NOROW = (VAR & 2048) != 0;
+  constexpr int GLS = WN * 2 / 16, GLZ = WN / 32;   // lanes carrying scales / zero words
+  constexpr int GPB = GR ? (GLS + GLZ) * 16 : 0;
+  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB + (GR ? NW : 0);
   constexpr int NPW = (NT + NW - 1) / NW;
-  constexpr int STAGE = A_BYTES + NB * 1024;
+  constexpr int GRB = NW * GPB;
+  constexpr int STAGE = A_BYTES + NB * 1024 + GRB;
   constexpr int KPP = 4 / NPH;
   // K tile kt+LA is staged during tile kt (slot of tile kt+LA-STAGES, last read during tile kt-1
   // at the latest), its pieces issued behind the MFMA bursts: a wave's MFMA half of phase 0
@@ -958,6 +981,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // lgkmcnt wait on its last reads of tile kt-1 (whose slot is restaged), so every read of the
   // slot has completed.
   constexpr bool DMA_LOAD = (VAR & 32) != 0;
+  static_assert(!(GR && DMA_LOAD), "grouped ping-pong: DMA behind the MFMA bursts only");
   constexpr int PRE_LAST = DMA_LOAD ? 0 : pp2_pre(NPH - 1, NPW, NPH, 0);
   // VAR & 16: v_mfma_f32_16x16x32_f16 fragments (same tile, LDS bytes and unpack count; the chip
   // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
@@ -977,7 +1001,9 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  // VAR & 4096 (and GR): the wave index -- hence piece choices and addresses -- in an SGPR
+  constexpr bool RFL = GR || (VAR & 4096) != 0;
+  const int wave = RFL ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int wm = wave / WAVES_N;
   const int wn = wave % WAVES_N;
   const int grp = wave >> 2;
@@ -992,11 +1018,26 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   const char* src[NPW];
   int dst[NPW];
   int step[NPW];
+  // VAR & 8192 (and GR): pieces dealt j = i * 8 + wave (interleaved) instead of wave * NPW + i;
+  // GR: slot NPW - 1 of wave w is w's group row (j = NA + NB + w)
+  constexpr bool ILV = GR || (VAR & 8192) != 0;
+  static_assert(!GR || ((NA + NB) % NW == 0 && NPW == (NA + NB) / NW + 1), "group row slot");
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
-    int j = wave * NPW + i;
+    int j = ILV ? i * NW + wave : wave * NPW + i;
     j = j < NT ? j : NT - 1;
-    if (j < NA) {
+    if (GR && i == NPW - 1) {
+      const int c0 = n0 + wn * WN;   // the wave's columns
+      if (lane < GLS) {
+        src[i] = (const char*)(scales + c0 + 8 * lane);
+        step[i] = N * 2;
+      } else {
+        const int l = lane - GLS < GLZ ? lane - GLS : 0;
+        src[i] = (const char*)(qzeros + c0 / 8 + 4 * l);
+        step[i] = (N / 8) * 4;
+      }
+      dst[i] = A_BYTES + NB * 1024 + wave * GPB;
+    } else if (j < NA) {
       const int row = j * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
       int gr = m0 + row;
@@ -1014,9 +1055,31 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   auto issue = [&](int kt, int slot, int i0, int i1) {
 #pragma unroll
     for (int i = 0; i < NPW; ++i)
-      if (i >= i0 && i < i1)
-        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)kt * step[i]),
-                                         (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+      if (i >= i0 && i < i1) {
+        if (GR && i == NPW - 1) {
+          if (!G_NOROW && lane < GLS + GLZ)
+            __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)(kt / kpg) * step[i]),
+                                             (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+        } else {
+          __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)kt * step[i]),
+                                           (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+        }
+      }
+  };
+  // GR: the raw group row values of this lane's columns (read after the retire wait of their tile)
+  // and the fp16 scale splats (set from them where a group starts)
+  half2_t gsc[TN], gsc16[TN][2];
+  uint32_t graw_s[TN][2], graw_z[TN][2];
+  auto gread = [&](int slot_) {
+    const char* gp = smem + slot_ * STAGE + A_BYTES + NB * 1024 + wave * GPB;
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < (M16 ? 2 : 1); ++h) {
+        const int cl = M16 ? 32 * t + 16 * h + (lane & 15) : 32 * t + (lane & 31);
+        graw_s[t][h] = *(const uint16_t*)(gp + 2 * cl);
+        graw_z[t][h] = *(const uint32_t*)(gp + WN * 2 + 4 * (cl >> 3)) >> (4 * (cl & 7));
+      }
   };
 
   int col[TN];
@@ -1084,6 +1147,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   for (int j = 0; j < LA; ++j)
     if (j < pro) issue(j, j, 0, NPW);
   vm_wait_le<(LA - 1) * NPW>((pro - 1) * NPW);
+  if (GR && !G_NOROW) gread(0);   // this wave's own group piece of tile 0 (its vmcnt wait covers it)
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -1096,6 +1160,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     tprev = t;
   };
   int slot = 0;
+  int gk = 0;   // GR: K tiles since the current group's first
   for (int kt = 0; kt < kt_count; ++kt) {
     const char* st = smem + slot * STAGE;
     const int ahead = kt + LA;
@@ -1112,6 +1177,22 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
         for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
         vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+        // tile kt+1 starts a group: its row (this wave's own piece, just retired) into registers
+        if (GR && !G_NOROW && gk + 1 == kpg) gread(slot + 1 == STAGES ? 0 : slot + 1);
+      }
+      if (GR && !G_NOROW && p == 0 && gk == 0) {   // first K tile of a group: its scale / zero splats
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int h = 0; h < (M16 ? 2 : 1); ++h) {
+            // fp16 bits: 1024 + zp = 0x6400 + zp, 64 + zp = 0x5400 + 16 zp (exact), splatted
+            const uint32_t zp = (graw_z[t][h] & 0xFu) + 1u;
+            W4Zero z;
+            z.z1024 = __builtin_bit_cast(half2_t, (0x6400u + zp) * 0x10001u);
+            z.z64 = __builtin_bit_cast(half2_t, (0x5400u + 16u * zp) * 0x10001u);
+            const half2_t sc2 = __builtin_bit_cast(half2_t, graw_s[t][h] * 0x10001u);
+            if constexpr (M16) { zc16[t][h] = z; gsc16[t][h] = sc2; } else { zc[t] = z; gsc[t] = sc2; }
+          }
       }
       if (M16 && p == 0) {
 #pragma unroll
@@ -1137,7 +1218,10 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
           for (int t = 0; t < TN; ++t)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) bf16[t][h][s] = w4_unpack(bw16[t][h][k32], ku, zc16[t][h]);
+            for (int h = 0; h < 2; ++h) {
+              bf16[t][h][s] = w4_unpack(bw16[t][h][k32], ku, zc16[t][h]);
+              if (GR && !G_NOSCALE) bf16[t][h][s] = scale8(bf16[t][h][s], gsc16[t][h]);
+            }
         }
       }
       half8_t af[TM][KPP];
@@ -1151,7 +1235,10 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
         for (int t = 0; t < TN; ++t)
 #pragma unroll
-          for (int s = 0; s < KPP; ++s) bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
+          for (int s = 0; s < KPP; ++s) {
+            bf[t][s] = w4_unpack(bw[t][p * KPP + s], ku, zc[t]);
+            if (GR && !G_NOSCALE) bf[t][s] = scale8(bf[t][s], gsc[t]);
+          }
       }
       if (DMA_LOAD && pf && p == NPH - 1) issue(ahead, sa, 0, NPW);
       if (VAR & 4) stamp(0);
@@ -1198,6 +1285,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       if (VAR & 4) stamp(3);
     }
     slot = slot == STAGES - 1 ? 0 : slot + 1;
+    if (GR) gk = gk + 1 == kpg ? 0 : gk + 1;
   }
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
   if ((VAR & 4) && lane == 0) {
@@ -1249,7 +1337,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int c = n0 + wn * WN + 32 * t + 16 * h + ql;
-        csc16[t][h] = (float)scales[c];
+        csc16[t][h] = GR ? 1.0f : (float)scales[c];
         cb16[t][h] = bias ? (float)bias[c] : 0.0f;
       }
     __syncthreads();
@@ -1260,7 +1348,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   float csc[TN], cb[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
-    csc[t] = (float)scales[col[t]];
+    csc[t] = GR ? 1.0f : (float)scales[col[t]];
     cb[t] = bias ? (float)bias[col[t]] : 0.0f;
   }
   __syncthreads();
@@ -1306,22 +1394,31 @@ static int launch_pp2(const GemmArgs& a, hipStream_t st) {
   constexpr int BM = WMW * TM * 32, BN = (8 / WMW) * TN * 32;
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
-                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K);
+                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64);
   SAMQ_LAUNCH_CHECK("w4a16_gemm_pp2 launch");
   return SAMQ_OK;
 }
 
 template <int EPI, bool GR>
 static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
-  if (cfg >= 50 && cfg < 80) {   // ping-pong kernels: per-channel scales only (groupsize == K)
-    if (GR) return fail(SAMQ_ERR_INVALID, "w4a16_gemm: ping-pong configs need groupsize == K");
+  if (cfg >= 50 && cfg < 100) {   // ping-pong kernels
+    if (GR) {   // grouped weights: the per-group scale / zero row rides in the ring (VAR & 512)
+      switch (cfg) {
+        // 3 slots, lookahead 2: four 40 KiB stages fill the 160 KiB LDS, the group row needs 640 B more
+        case 57: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
+        case 64: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16>(a, st);   // (slower than 57 on every shape)
+        default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: grouped weights take ping-pong configs 57 / 64 only");
+      }
+    }
     switch (cfg) {
       case 55: return launch_pp2<2, 4, 2, 2, 3, 2, EPI>(a, st);   // v6 256x256, 2 k-phases, 3 slots
       case 56: return launch_pp2<2, 4, 2, 2, 4, 2, EPI>(a, st);   // 4 slots, lookahead 2 (DMA in both phases)
-      case 57: return launch_pp2<2, 4, 2, 2, 4, 3, EPI>(a, st);   // 4 slots, lookahead 3
+      // 4 slots, lookahead 3; the wave index in an SGPR (VAR & 4096: uniform piece addressing,
+      // -3..-6 % isolated vs the VGPR form at M = 8192, profiles/r3_gemm_rfl.log)
+      case 57: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
       case 58: return launch_pp2<2, 4, 2, 1, 4, 2, EPI>(a, st);   // 1 phase / K tile, 4 slots, lookahead 2
       case 62: return launch_pp2<4, 2, 4, 2, 4, 3, EPI>(a, st);   // 4x2 waves (64x128 each): A read 2x, B 4x
-      case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16>(a, st);  // cfg 57 on 16x16x32 MFMA
+      case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);  // cfg 57 on 16x16x32 MFMA
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
 #ifdef SAMQ_TUNING
       // tuning build only (make tuning): untested shapes and TIMING-ONLY variants that compute
@@ -1346,6 +1443,26 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 54: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 256>(a, st);
       case 59: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 272>(a, st);
       case 70: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 1>(a, st);   // timing-only: cfg 57 without restaging
+      // grouped timing-only (per-channel weights, grouped code path): 74 / 75 = 57g without the
+      // fp16 group scaling / without the group row; 76 / 77 the same on 64g
+      case 74: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 1024>(a, st);
+      case 75: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 2048>(a, st);
+      case 76: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16 | 1024>(a, st);
+      case 77: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16 | 2048>(a, st);
+      case 78: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);        // 57g on per-channel weights
+      case 79: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16>(a, st);   // 64g on per-channel weights
+      // per-channel: wave index in an SGPR (90), interleaved piece deal (91), both (92 / 93 on 16x16)
+      case 90: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
+      case 91: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 8192>(a, st);
+      case 92: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 8192>(a, st);
+      case 93: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 8192>(a, st);
+      case 94: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);
+      case 95: return launch_pp2<2, 4, 2, 2, 4, 3, EPI>(a, st);       // round-2 cfg 57 (VGPR wave index)
+      case 96: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16>(a, st);   // round-2 cfg 64
+      // 1x8 waves of 128x64: 128x512 tiles, A staged once per 512 columns (32 instead of 40 LDS-DMA
+      // pieces per 256x256-equivalent of work); N % 512 == 0 (lin1)
+      case 97: return launch_pp2<1, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
+      case 98: return launch_pp2<1, 4, 2, 2, 5, 4, EPI, 4096>(a, st);
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
       case 73: {   // timing experiment: cfg 57 with per-segment s_memtime stamps (synchronous)
@@ -1418,7 +1535,9 @@ static int pick_cfg(int M, int N, bool grouped) {
   // 1161 TF/s there vs 969 on the one-round 128x320 tiles (cfg 29) that win an isolated M = 8192
   // launch, and inside the 2-lane graph -- where the other lane fills any tail -- the step drops
   // 25.66 -> 24.35 ms with bit-identical output (profiles/r2_cfg_ab.log)
-  if (!grouped && N % 256 == 0 && M >= 8192) return N >= 2048 ? 57 : 64;
+  // grouped weights: the 32x32x16 ping-pong with the group rows in the ring (VAR & 512) for every
+  // N (its 16x16x32 twin is 6-13 % slower on all four shapes, profiles/r3_gemm_grouped.log)
+  if (N % 256 == 0 && M >= 8192) return grouped || N >= 2048 ? 57 : 64;
   if (N % 256 == 0 && M >= 1024) return 22;
   if (N % 128 == 0 && M >= 512) return 23;
   if (N % 64 == 0) return 26;
@@ -1436,6 +1555,9 @@ static int cfg_bn(int cfg) {
                  case 52: return 256; case 53: return 256; case 54: return 256; case 59: return 256; case 55: return 256; case 56: return 256; case 57: return 256; case 58: return 256;
                  case 60: return 256; case 61: return 256; case 62: return 256; case 64: return 256; case 65: return 256; case 68: return 256; case 69: return 256; case 66: return 256; case 67: return 256;
                  case 70: return 256; case 71: return 256; case 72: return 256; case 73: return 256;
+                 case 74: case 75: case 76: case 77: case 78: case 79: return 256;
+                 case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
+                 case 97: case 98: return 512;
                  default: return 0; }
 }
 

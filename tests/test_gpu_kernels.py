@@ -112,10 +112,26 @@ def test_w4a16_gemm_pingpong(cuda, cfg, epi):
         _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, -1, epi, cfg, rng)
 
 
+@pytest.mark.parametrize("cfg", [57, 64])
+@pytest.mark.parametrize("groupsize", [64, 128, 256])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
+def test_w4a16_gemm_pingpong_grouped(cuda, cfg, groupsize, epi):
+    """Grouped weights on the ping-pong kernels (the group's scale / zero row staged with every K
+    tile, fp16((q - zp) * s) in the unpack; reference quant_linear.py:324-335): ragged M, K of
+    1 .. 40 K tiles, every epilogue, against the oracle."""
+    from samq import ops
+    for m, k, n in ((333, 1280, 512), (300, max(64, groupsize), 256), (260, 3 * groupsize, 256), (513, 2560, 768)):
+        qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=cfg * 17 + k + groupsize)
+        rng = np.random.Generator(np.random.PCG64(cfg + k + groupsize))
+        a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+        y = gptq_pack.matmul4_g1(a, qw, sc, qz, groupsize, bias)
+        _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, groupsize, epi, cfg, rng)
+
+
 @pytest.mark.parametrize("groupsize", [-1, 128])
 def test_w4a16_gemm_auto_pick_wide(cuda, groupsize):
-    """The automatic tile choice at the ViT-H wide shapes (M >= 4096, N >= 2048: ping-pong v6 for
-    per-channel weights, v3 for grouped ones) against the oracle."""
+    """The automatic tile choice below one 2-image lane (M = 4133: the v3 128x256 tiles) at a
+    ViT-H wide shape, per-channel and grouped, against the oracle."""
     from samq import ops
     m, k, n = 4133, 1280, 2304
     qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=77 + (groupsize > 0))
@@ -128,22 +144,23 @@ def test_w4a16_gemm_auto_pick_wide(cuda, groupsize):
 
 
 @pytest.mark.parametrize("n", [1280, 2560])
-def test_w4a16_gemm_auto_pick_lane(cuda, n):
+@pytest.mark.parametrize("groupsize", [-1, 128])
+def test_w4a16_gemm_auto_pick_lane(cuda, n, groupsize):
     """The automatic tile choice at one 2-image lane (M = 8192): the 16x16x32 ping-pong (cfg 64)
-    for the N = 1280 projections, the 32x32x16 one (cfg 57) for wide N -- against the oracle, and
-    bit-identical to the explicit config."""
+    for the N = 1280 projections, the 32x32x16 one (cfg 57) for wide N, per-channel and grouped
+    -- against the oracle, and bit-identical to the explicit config."""
     from samq import ops
     m, k = 8192, 1280
-    qw, qz, sc, bias = _packed_layer(k, n, -1, seed=91 + n)
+    qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=91 + n + groupsize)
     rng = np.random.Generator(np.random.PCG64(92))
     a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
-    y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
+    y = gptq_pack.matmul4_g1(a, qw, sc, qz, groupsize, bias)
     packed = ops.w4_repack(_dev(qw, cuda))
     for epi in ("bias", "resadd"):
-        _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, -1, epi, 0, rng)
-    args = (_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, -1)
+        _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, 0, rng)
+    args = (_dev(a, cuda), packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, groupsize)
     auto = ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=0)
-    assert torch.equal(auto, ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=64 if n < 2048 else 57))
+    assert torch.equal(auto, ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=64 if n < 2048 and groupsize == -1 else 57))
 
 
 @pytest.mark.parametrize("tag", ["gm1", "g128"])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--shapes", default="qkv,proj,lin1,lin2")
     ap.add_argument("--epi", default="native", help="native | bias (force EPI_BIAS)")
     ap.add_argument("--torch", action="store_true", help="also time dense fp16 torch.matmul")
+    ap.add_argument("--groupsize", type=int, default=-1)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -39,9 +40,10 @@ def main():
         k, n, epi = SHAPES[name]
         if args.epi == "bias":
             epi = ops.EPI_BIAS
-        q = QuantLinear(4, -1, k, n, True).to(dev)
+        gs = args.groupsize
+        q = QuantLinear(4, gs, k, n, True).to(dev)
         w = torch.randn(n, k, device=dev) * 0.02
-        fake, s, z = rtn(w)
+        fake, s, z = rtn(w, gs)
         pack_linear(q, fake, s, z, torch.randn(n, device=dev) * 0.02)
         packed = q.prepare()
         # layout-2 weights exist only in the tuning build (SAMQ_LIB=tuning, make tuning)
@@ -53,7 +55,7 @@ def main():
         for c in cfgs + [3]:
             out = torch.zeros(m, n, device=dev, dtype=torch.float32 if f32 else torch.float16)
             try:
-                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=out, cfg=c)
+                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, gs, epi, out=out, cfg=c)
             except AssertionError as e:
                 print(f"{name} cfg {c}: skipped ({e})")
                 continue
@@ -65,10 +67,10 @@ def main():
         for _ in range(3):
             for c in outs:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
+                ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, gs, epi, out=outs[c], cfg=c)
                 e0.record(stream)
                 for _ in range(args.iters):
-                    ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=outs[c], cfg=c)
+                    ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, gs, epi, out=outs[c], cfg=c)
                 e1.record(stream)
                 torch.cuda.synchronize()
                 times[c].append(e0.elapsed_time(e1) / args.iters * 1e3)
@@ -77,9 +79,9 @@ def main():
             us = min(times[c])
             # residual epilogues accumulate: compare a fresh single launch instead
             o = torch.zeros_like(outs[c])
-            ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, -1, epi, out=o, cfg=c)
+            ops.w4a16_gemm(a, pk(c), q.scales, q.qzeros, q.bias, n, gs, epi, out=o, cfg=c)
             r = torch.zeros_like(outs[3])
-            ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, -1, epi, out=r, cfg=3)
+            ops.w4a16_gemm(a, packed, q.scales, q.qzeros, q.bias, n, gs, epi, out=r, cfg=3)
             err = (o.float() - r.float()).abs().max().item()
             print(f"{name:5s} M={m} K={k} N={n} cfg {c}: {us:8.1f} us  {flops / us / 1e6:7.1f} TF/s  "
                   f"({flops / us / 1e6 / 2500 * 100:4.1f}% fp16 peak)  maxdiff vs cfg3 {err:.2e}")

@@ -33,6 +33,9 @@ for step in "$@"; do
     b88q)    run b88q 400 python bench.py --mode w8a8 --steps 20 --warmup 5 --no-cpu-baseline ;;
     benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
     instep)  run instep 500 bash tools/instep_profile.sh w4a16 ;;
+    benchg)  run benchg 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --groupsize 128 ;;
+    instepg) run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128 ;;
+    grouped) run grouped 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rA -k "grouped or auto_pick or configs" ;;
     instep48) run instep48 500 bash tools/instep_profile.sh w4a8 ;;
     instepb8) run instepb8 500 bash tools/instep_profile.sh w4a16 --batch 8 ;;
     instep88) run instep88 500 bash tools/instep_profile.sh w8a8 ;;

@@ -22,7 +22,7 @@ import bench
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
 c = d["config"]
-print(f"instep_{sys.argv[1]}_b{c['per_gpu_batch'] // c['lanes']}_l{c['lanes']}_{bench.source_hash()}")
+print(bench.instep_name(sys.argv[1], c['per_gpu_batch'] // c['lanes'], c['lanes'], c.get('groupsize', -1)))
 PY
 )
 python3 tools/instep_window.py "$d" $steps "gpurun_out/$name.json" "$mode"
