@@ -952,21 +952,22 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   constexpr int BM = WAVES_M * WM, BN = WAVES_N * WN;
   constexpr int BK = 64, ROWB = BK * 2;
   constexpr int A_BYTES = BM * ROWB;
-  // VAR & 512: grouped weights (groupsize = 64 kpg < K).  Every wave stages, with each K tile, one
-  // more LDS-DMA piece: the group row of ITS OWN WN columns -- WN fp16 scales (lanes 0 .. WN/8-1) and
-  // WN/8 packed zero words (the next WN/32 lanes; the rest idle), GPB bytes -- so the wave's own
-  // retire wait covers it (no barrier): it reads tile kt+1's row right after that wait in tile kt's
-  // last load half and converts it in tile kt+1's phase 0 (only where a new group starts).  The
-  // unpack scales the exact integers once in fp16, fp16((q - zp) * s) (the v3 kernels' semantics),
-  // and the epilogue's per-channel scale is 1.
+  // VAR & 512: grouped weights (groupsize = 64 kpg < K).  The K tile that starts a group carries
+  // one more LDS-DMA piece, the group row of the whole tile: BN fp16 scales (lanes 0 .. BN/8-1) and
+  // BN/8 packed zero words (the next BN/32 lanes; the rest idle), GRB bytes behind the B pieces.
+  // Wave 0 issues it (compile-time slot NPW - 1, in the last phase); every wave reads its columns
+  // of tile kt+1's row in the MFMA half of tile kt's last phase -- after the barrier that follows
+  // every wave's retire wait for tile kt+1, wave 0's included -- and converts them in tile kt+1's
+  // phase 0.  The unpack scales the exact integers once in fp16, fp16((q - zp) * s) (the v3
+  // kernels' semantics); the epilogue's per-channel scale is 1.
   constexpr bool GR = (VAR & 512) != 0;
   // timing-only (tuning build): VAR & 1024 skips the fp16 group scaling, VAR & 2048 the group row
   constexpr bool G_NOSCALE = (VAR & 1024) != 0, G_NOROW = (VAR & 2048) != 0;
-  constexpr int GLS = WN * 2 / 16, GLZ = WN / 32;   // lanes carrying scales / zero words
-  constexpr int GPB = GR ? (GLS + GLZ) * 16 : 0;
-  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB + (GR ? NW : 0);
+  constexpr int GLS = BN * 2 / 16, GLZ = BN / 32;   // lanes carrying scales / zero words
+  static_assert(!GR || GLS + GLZ <= 64, "group row: one lane per 16 bytes");
+  constexpr int GRB = GR ? (GLS + GLZ) * 16 : 0;
+  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB + (GR ? 1 : 0);
   constexpr int NPW = (NT + NW - 1) / NW;
-  constexpr int GRB = NW * GPB;
   constexpr int STAGE = A_BYTES + NB * 1024 + GRB;
   constexpr int KPP = 4 / NPH;
   // K tile kt+LA is staged during tile kt (slot of tile kt+LA-STAGES, last read during tile kt-1
@@ -1019,24 +1020,24 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   int dst[NPW];
   int step[NPW];
   // VAR & 8192 (and GR): pieces dealt j = i * 8 + wave (interleaved) instead of wave * NPW + i;
-  // GR: slot NPW - 1 of wave w is w's group row (j = NA + NB + w)
+  // GR: the A / B pieces fill slots i < NPW - 1; slot NPW - 1 of wave 0 is the group row
   constexpr bool ILV = GR || (VAR & 8192) != 0;
   static_assert(!GR || ((NA + NB) % NW == 0 && NPW == (NA + NB) / NW + 1), "group row slot");
+  static_assert(!GR || pp2_pre(NPH - 1, NPW, NPH, 0) <= NPW - 1, "group row issued in the last phase");
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     int j = ILV ? i * NW + wave : wave * NPW + i;
     j = j < NT ? j : NT - 1;
     if (GR && i == NPW - 1) {
-      const int c0 = n0 + wn * WN;   // the wave's columns
       if (lane < GLS) {
-        src[i] = (const char*)(scales + c0 + 8 * lane);
+        src[i] = (const char*)(scales + n0 + 8 * lane);
         step[i] = N * 2;
       } else {
         const int l = lane - GLS < GLZ ? lane - GLS : 0;
-        src[i] = (const char*)(qzeros + c0 / 8 + 4 * l);
+        src[i] = (const char*)(qzeros + n0 / 8 + 4 * l);
         step[i] = (N / 8) * 4;
       }
-      dst[i] = A_BYTES + NB * 1024 + wave * GPB;
+      dst[i] = A_BYTES + NB * 1024;
     } else if (j < NA) {
       const int row = j * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((row >> 1) & 7);
@@ -1057,9 +1058,12 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     for (int i = 0; i < NPW; ++i)
       if (i >= i0 && i < i1) {
         if (GR && i == NPW - 1) {
-          if (!G_NOROW && lane < GLS + GLZ)
-            __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)(kt / kpg) * step[i]),
-                                             (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+          // wave 0, and only for a K tile that starts a group (uniform: wave is an SGPR)
+          if (!G_NOROW && wave == 0 && kt % kpg == 0) {
+            if (lane < GLS + GLZ)
+              __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)(kt / kpg) * step[i]),
+                                               (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
+          }
         } else {
           __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src[i] + (int64_t)kt * step[i]),
                                            (SAMQ_LDS void*)(smem + slot * STAGE + dst[i]), 16, 0, 0);
@@ -1071,16 +1075,18 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   half2_t gsc[TN], gsc16[TN][2];
   uint32_t graw_s[TN][2], graw_z[TN][2];
   auto gread = [&](int slot_) {
-    const char* gp = smem + slot_ * STAGE + A_BYTES + NB * 1024 + wave * GPB;
+    const char* gp = smem + slot_ * STAGE + A_BYTES + NB * 1024;
 #pragma unroll
     for (int t = 0; t < TN; ++t)
 #pragma unroll
       for (int h = 0; h < (M16 ? 2 : 1); ++h) {
-        const int cl = M16 ? 32 * t + 16 * h + (lane & 15) : 32 * t + (lane & 31);
+        const int cl = wn * WN + (M16 ? 32 * t + 16 * h + (lane & 15) : 32 * t + (lane & 31));
         graw_s[t][h] = *(const uint16_t*)(gp + 2 * cl);
-        graw_z[t][h] = *(const uint32_t*)(gp + WN * 2 + 4 * (cl >> 3)) >> (4 * (cl & 7));
+        graw_z[t][h] = *(const uint32_t*)(gp + BN * 2 + 4 * (cl >> 3)) >> (4 * (cl & 7));
       }
   };
+  // GR: LDS-DMA pieces this wave issues for K tile t (wave 0 adds the group row where a group starts)
+  auto npieces = [&](int t) -> int { return GR ? NPW - 1 + (wave == 0 && t % kpg == 0 ? 1 : 0) : NPW; };
 
   int col[TN];
   W4Zero zc[TN];
@@ -1146,9 +1152,14 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
   for (int j = 0; j < LA; ++j)
     if (j < pro) issue(j, j, 0, NPW);
-  vm_wait_le<(LA - 1) * NPW>((pro - 1) * NPW);
-  if (GR && !G_NOROW) gread(0);   // this wave's own group piece of tile 0 (its vmcnt wait covers it)
+  {
+    int newer = 0;
+#pragma unroll
+    for (int j = 1; j < LA; ++j) newer += j < pro ? npieces(j) : 0;
+    vm_wait_le<(LA - 1) * NPW>(newer);
+  }
   __builtin_amdgcn_s_barrier();
+  if (GR && !G_NOROW) gread(0);   // tile 0's row: wave 0's retire wait precedes the barrier above
   if (grp) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
@@ -1175,10 +1186,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
         // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
         int newer = pf ? PRE_LAST : 0;
 #pragma unroll
-        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
+        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? npieces(kt + j) : 0;
         vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
-        // tile kt+1 starts a group: its row (this wave's own piece, just retired) into registers
-        if (GR && !G_NOROW && gk + 1 == kpg) gread(slot + 1 == STAGES ? 0 : slot + 1);
       }
       if (GR && !G_NOROW && p == 0 && gk == 0) {   // first K tile of a group: its scale / zero splats
 #pragma unroll
@@ -1277,6 +1286,10 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
       // the barrier otherwise; WAR-safe in every phase: see header)
       if (pf && !DMA_LOAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
+      // GR: tile kt+1 starts a group -> its row into registers (every wave's retire wait for tile
+      // kt+1, wave 0's included, precedes the barrier that opened this MFMA half)
+      if (GR && !G_NOROW && p == NPH - 1 && kt + 1 < kt_count && gk + 1 == kpg)
+        gread(slot + 1 == STAGES ? 0 : slot + 1);
       if (VAR & 4) stamp(2);
       if (!(VAR & 256)) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
