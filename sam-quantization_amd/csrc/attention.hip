@@ -27,6 +27,8 @@
 //    query of the wave raised its max (alpha == 1 exactly, bit-identical results).
 #include "common.h"
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace samq {
@@ -56,6 +58,7 @@ struct AttnParams {
   int nwx, upi;             // windows per row, windows per image
   float scale;              // sm_scale
   int nqb, units;           // streaming path with a 1-D XCD-ordered grid: query blocks, units
+  int dbg;                  // tuning build only: timing experiments (0 in the product)
   float out_scale, out_inv; // > 0: out holds int8 codes q8(fp16(o), out_scale) (W4A8 proj QAct)
 };
 
@@ -833,6 +836,392 @@ __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int
   }
 }
 
+// ------------------------------------------------------------------ global attention, 32x32 MFMA
+// ViT-H global blocks (64 x 64 grid, head dim 80) on v_mfma_f32_32x32x16_f16: the 32x32 form
+// issues half the MFMA instructions per FLOP of 16x16x32 (each holds the SIMD's vector issue for
+// 8 of its 32 cycles, MI355X_MICROARCH.md constants) and D = 80 is 5 k16-steps, no padding.
+//  * a wave owns one query tile of 32 queries of ONE grid row qh (so the width table row
+//    qh - kw + 63 is one A operand for the whole tile: reference quirk 1 keeps both tables on qh);
+//    8 waves = 4 grid rows per workgroup, 16 workgroups per (image, head), one workgroup per CU;
+//  * key row kh (64 keys) = two 32-key tiles: S^T = K.Q^T + TW (5 MFMAs each, TW[kt] = log2e q.Rw
+//    as the C input, computed once per tile by the same MFMA form); TH[q, kh] = log2e q.Rh, fp16-
+//    rounded like the reference's rel_h, kept per wave in LDS and folded into the running max;
+//  * a lane holds 32 scores of ONE query (its partner lane ^ 32 the other 32): the row max is
+//    in-register + one cross-lane step; lazy exp2 offset (moves only past +8); P stays in the
+//    score registers' order, which IS the B operand of O^T += V^T . P^T (k-slot 8h + j <-> key
+//    16u + 4h + j (j < 4) / 16u + 8 + 4h + j - 4);
+//  * V^T fragments by ds_read_b64_tr_b16 from 4-key x 32-dim chunks (256 contiguous bytes per
+//    read group: conflict-free); d-block 2 covers dims 64..95, its rows 80..95 forced to 1.0 so
+//    the same MFMAs produce the softmax row sums (no extra MFMA, no VALU sum);
+//  * K pieces lane-linear (lane l of piece (kt, s) = key 32 kt + l % 32, dims 16 s + 8 (l / 32):
+//    the A fragment read is ds_read_b128 at l * 16); key rows stream through a 3-deep LDS ring
+//    (20 KiB per row, LDS-DMA, 20 pieces over 8 waves), one barrier per key row, the next row's
+//    Q.K^T MFMAs issued ahead of the current row's softmax.
+__device__ __forceinline__ float16_t mfma32(half8_t a, half8_t b, float16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+#ifdef SAMQ_TUNING
+__device__ unsigned long long g_attn_stamps[8];   // timing experiments (tuning build)
+#endif
+
+__global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) {
+  constexpr int D = 80, S = 64, KS = 5;
+  constexpr int NSLOT = 5;                        // key-row ring slots
+  constexpr int ROWB = 20 * 1024;                 // one key row: K (10 KiB) | V (10 KiB)
+  constexpr int VB = 10 * 1024;
+  constexpr int THB = 64 * 32 * 2;                // per wave: fp16 TH[kh][q]
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 8 * THB];
+#ifdef SAMQ_TUNING
+  const bool DBG_NOEXP = (p.dbg & 2) != 0, DBG_NOMFMA = (p.dbg & 4) != 0;
+#else
+  constexpr bool DBG_NOEXP = false, DBG_NOMFMA = false;
+#endif
+
+  _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;                       // waves w, w + 4 share a SIMD
+  const int l32 = lane & 31, h = lane >> 5;
+  // XCD-aware 1-D grid: the 16 query blocks of one (image, head) on one XCD (shared K/V in its L2)
+  const int nqb = p.nqb, pairs = p.heads * p.units;
+  const int xcd = blockIdx.x & 7, kk = blockIdx.x >> 3;
+  const int pair = xcd * (pairs >> 3) + kk / nqb;
+  const int qblk = kk % nqb;
+  const int head = pair % p.heads;
+  const int b = pair / p.heads;
+  const int C = p.C;
+  const int qh = 4 * qblk + (wave >> 1);           // this wave's query grid row
+  const int qw0 = 32 * (wave & 1);
+  const _Float16* img = p.qkv + (int64_t)b * S * S * p.tok_stride;
+
+  // ---- K / V staging: 20 pieces per key row; wave w issues pieces w, w + 8 (, w + 16 for w < 4)
+  constexpr int NI = 3;
+  const int npc = wave < 4 ? 3 : 2;
+  const _Float16* src0[NI];
+  int dst[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int v = wave + 8 * i;
+    int key, dim;
+    if (v < 10) {                                  // K piece (kt, s): lane-linear A fragments
+      key = 32 * (v / 5) + l32;
+      dim = C + 16 * (v % 5) + 8 * h;
+    } else {                                       // V: 16 key-quads x (256 + 256 + 128 bytes)
+      const int gl = 64 * (v - 10) + lane;
+      const int kq = gl / 40, w = gl % 40;
+      if (w < 16)      { key = 4 * kq + (w >> 2);        dim = 2 * C + 8 * (w & 3); }
+      else if (w < 32) { key = 4 * kq + ((w - 16) >> 2); dim = 2 * C + 32 + 8 * (w & 3); }
+      else             { key = 4 * kq + ((w - 32) >> 1); dim = 2 * C + 64 + 8 * (w & 1); }
+      key = key < S ? key : S - 1;
+    }
+    src0[i] = img + (int64_t)key * p.tok_stride + head * D + dim;
+    dst[i] = v * 1024;
+  }
+  const int64_t rowstride = (int64_t)S * p.tok_stride;
+  auto issue = [&](int kh, int slot) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if (i < npc)
+        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src0[i] + kh * rowstride),
+                                         (SAMQ_LDS void*)(smem + slot * ROWB + dst[i]), 16, 0, 0);
+  };
+#pragma unroll
+  for (int r = 0; r < NSLOT - 1; ++r) issue(r, r);
+
+  // ---- Q^T fragments (B operand): lane = query qw0 + l32, dims 16 s + 8 h (fp16(q * scale * log2e))
+  const float qscale = p.scale * LOG2E;
+  half8_t qf[KS];
+  {
+    const _Float16* qp = img + ((int64_t)qh * S + qw0 + l32) * p.tok_stride + head * D + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      half8_t v = *(const half8_t*)(qp + 16 * s);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (_Float16)__builtin_fmaf((float)v[j], qscale, 0.0f);
+      qf[s] = v;
+    }
+  }
+  // ---- rel-pos terms: TW[kt] (score layout, the C input) and TH -> LDS (fp16, per wave)
+  const float inv_scale = 1.0f / p.scale;
+  float16_t tw[2];
+  _Float16* thw = th_lds + wave * (64 * 32);
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+    const _Float16* tab = which ? p.relw : p.relh;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const int r = qh - (32 * kt + l32) + S - 1;   // table row of this lane's A row (key column / key row)
+      const _Float16* rp = tab + (int64_t)r * D + 8 * h;
+      float16_t a = {};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a = mfma32(*(const half8_t*)(rp + 16 * s), qf[s], a);
+      a = a * inv_scale;
+      if (which) {
+        tw[kt] = a;
+      } else {
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) {
+          const int kh = 32 * kt + 8 * (r2 >> 2) + 4 * h + (r2 & 3);
+          thw[kh * 32 + l32] = (_Float16)a[r2];
+        }
+      }
+    }
+  }
+
+  // ---- V^T fragment addresses (ds_read_b64_tr_b16): lane 4q + p of its 16-lane group reads
+  // key 4 kq + q, dims 16 g16 + 4p .. of the chunk; d-block 2 lanes g16 = 1 (dims 80..95) read
+  // the g16 = 0 bytes and are forced to 1.0 below
+  const int i16 = lane & 15, g16 = (lane >> 4) & 1;
+  const int tq = i16 >> 2, tp = i16 & 3;
+  const uint32_t vb01 = lds_addr(smem + VB) + h * 640 + tq * 64 + g16 * 32 + tp * 8;
+  const uint32_t vb2 = lds_addr(smem + VB) + h * 640 + 512 + tq * 32 + tp * 8;
+  const uint32_t ones_or = g16 ? 0x3C003C00u : 0u, ones_and = g16 ? 0u : 0xFFFFFFFFu;
+
+  float16_t o[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) o[d] = float16_t{};
+  float m = -INFINITY;
+  float16_t sc[2];
+  half8_t pb[2][2];
+
+  half8_t kf[2][KS];
+  auto kread = [&](const char* kb) {   // K fragments of a key row (A operands, lane-linear pieces)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) kf[kt][s] = *(const half8_t*)(kb + (kt * 5 + s) * 1024 + lane * 16);
+  };
+  auto qk = [&]() {   // S^T = K . Q^T + TW for the two 32-key tiles of a key row
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      float16_t a = tw[kt];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (DBG_NOMFMA) a[s] += (float)kf[kt][s][0] * (float)qf[s][0];
+        else a = mfma32(kf[kt][s], qf[s], a);
+      }
+      sc[kt] = a;
+    }
+  };
+  // Online softmax (exp2 domain), lane = one query, 32 of its 64 keys.  P is computed with the
+  // offset m of the PREVIOUS rows, so the exp2s do not wait for this row's max (whose reduction +
+  // cross-lane step + compare is a serial chain): the max runs beside them and only decides
+  //  * m moves by > 8 (lazy offset): applied after this row's P.V, before the next row's P
+  //    (O *= exp2(m - m_new) there; P and O of this row share the old offset);
+  //  * this row's P could exceed 2^15 (fp16 range): rare slow path, O rescaled and P recomputed
+  //    with the new offset now (always taken for row 0, m = -inf).
+  float th_cur = (float)thw[l32];   // TH of row 0
+  float m_pend = -INFINITY;
+  bool pend = false;
+  auto softmax = [&](int kh) {
+    if (__any(pend)) {   // last row's deferred offset move
+      const float alpha = pend ? __builtin_amdgcn_exp2f(m - m_pend) : 1.0f;
+      m = pend ? m_pend : m;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) o[d] = o[d] * alpha;
+      pend = false;
+    }
+    float corr = m - th_cur;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[kt][u][j] = (_Float16)(DBG_NOEXP ? sc[kt][8 * u + j] - corr
+                                                                   : __builtin_amdgcn_exp2f(sc[kt][8 * u + j] - corr));
+    float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
+    float my = max3f(sc[1][0], sc[1][1], sc[1][2]);
+#pragma unroll
+    for (int r = 3; r + 1 < 16; r += 2) {
+      mx = max3f(mx, sc[0][r], sc[0][r + 1]);
+      my = max3f(my, sc[1][r], sc[1][r + 1]);
+    }
+    mx = max3f(mx, my, fmaxf(sc[0][15], sc[1][15]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mrow = mx + th_cur;
+    const bool unsafe = !(mrow <= m + 15.0f);   // (m = -inf: unsafe)
+    if (__any(unsafe)) {
+      const float mnew = unsafe ? mrow : m;
+      const float alpha = unsafe ? __builtin_amdgcn_exp2f(m - mnew) : 1.0f;
+      m = mnew;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) o[d] = o[d] * alpha;
+      corr = m - th_cur;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[kt][u][j] = (_Float16)__builtin_amdgcn_exp2f(sc[kt][8 * u + j] - corr);
+    }
+    pend = mrow > m + 8.0f;
+    m_pend = mrow;
+    if (kh + 1 < S) th_cur = (float)thw[(kh + 1) * 32 + l32];
+  };
+  // V^T fragments of k16-step t = (kt, u): six ds_read_b64_tr_b16 (lo / hi key quads x 3 d-blocks)
+  auto vread = [&](auto tc, uint32_t rb, half4_t (&lo)[3], half4_t (&hi)[3]) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int KQ = 8 * (t >> 1) + 4 * (t & 1);   // key quad of slot j < 4 (+h); j >= 4: +2
+    lo[0] = ds_read_tr16_off<KQ * 640>(vb01 + rb);
+    hi[0] = ds_read_tr16_off<(KQ + 2) * 640>(vb01 + rb);
+    lo[1] = ds_read_tr16_off<KQ * 640 + 256>(vb01 + rb);
+    hi[1] = ds_read_tr16_off<(KQ + 2) * 640 + 256>(vb01 + rb);
+    lo[2] = ds_read_tr16_off<KQ * 640>(vb2 + rb);
+    hi[2] = ds_read_tr16_off<(KQ + 2) * 640>(vb2 + rb);
+  };
+  auto pv = [&](int slot) {   // O^T += V^T . P^T: 4 k16-steps x 3 d-blocks, next step's reads in flight
+    const uint32_t rb = slot * ROWB;
+    half4_t lo[2][3], hi[2][3];
+    vread(std::integral_constant<int, 0>{}, rb, lo[0], hi[0]);
+    static_for<4>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int cb = t & 1;
+      if constexpr (t + 1 < 4) {
+        vread(std::integral_constant<int, t + 1>{}, rb, lo[cb ^ 1], hi[cb ^ 1]);
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(lo[cb][0]), "+v"(hi[cb][0]), "+v"(lo[cb][1]), "+v"(hi[cb][1]),
+                     "+v"(lo[cb][2]), "+v"(hi[cb][2]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[cb][0]), "+v"(hi[cb][0]), "+v"(lo[cb][1]), "+v"(hi[cb][1]),
+                     "+v"(lo[cb][2]), "+v"(hi[cb][2]));
+      }
+      {   // d-block 2, dims 80..95 -> 1.0 (row sums)
+        union { half4_t v; uint32_t w[2]; } a, c;
+        a.v = lo[cb][2];
+        c.v = hi[cb][2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          a.w[e] = (a.w[e] & ones_and) | ones_or;
+          c.w[e] = (c.w[e] & ones_and) | ones_or;
+        }
+        lo[cb][2] = a.v;
+        hi[cb][2] = c.v;
+      }
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const half8_t va = {lo[cb][d][0], lo[cb][d][1], lo[cb][d][2], lo[cb][d][3],
+                            hi[cb][d][0], hi[cb][d][1], hi[cb][d][2], hi[cb][d][3]};
+        if (DBG_NOMFMA) o[d][0] += (float)va[0] * (float)pb[t >> 1][t & 1][0];
+        else o[d] = mfma32(va, pb[t >> 1][t & 1], o[d]);
+      }
+    });
+  };
+
+  // ---- key-row loop as a two-group ping-pong (MI355X_MICROARCH.md "Two waves per SIMD"): per
+  // key row a VALU segment (softmax of row kh + the K fragment reads of row kh+1) and an MFMA
+  // segment (P.V of row kh, Q.K^T of row kh+1), one barrier apart; waves 4..7 (group 1) run one
+  // barrier behind waves 0..3, so each SIMD pairs one wave's softmax with its partner's MFMAs.
+  // Barrier n: group 0's VALU segment of row kh lies between barriers 2kh-1 and 2kh, its MFMA
+  // segment between 2kh and 2kh+1; group 1's one barrier later.  Ring of 5 slots, row r in slot
+  // r % 5:
+  //  * row kh+4 is staged at the start of the MFMA segment of row kh into row kh-1's slot, whose
+  //    last reads (group 1's P.V of row kh-1) ended at that segment's opening barrier;
+  //  * row r is first read by group 0's VALU segment of row r-1 (after barrier 2r-3), so every
+  //    wave retires its pieces of row r before barrier 2r-3: group 0 at the end of its MFMA
+  //    segment of row r-2, group 1 at the end of its VALU segment of row r-2.
+  // The asm fences pin the softmax results and K fragments to their segment (the compiler would
+  // otherwise sink the exp2s past the barrier into the MFMA segment).
+  auto retire = [&](int newer) {   // s_waitcnt vmcnt(newer) for a wave-uniform newer in {0, 2, 3, 4, 6}
+    if (newer >= 6) wait_vmcnt<6>();
+    else if (newer >= 4) wait_vmcnt<4>();
+    else if (newer >= 3) wait_vmcnt<3>();
+    else if (newer >= 2) wait_vmcnt<2>();
+    else wait_vmcnt<0>();
+  };
+  wait_vmcnt<0>();
+  __syncthreads();   // rows 0..3 landed; TH visible
+  kread(smem);
+  qk();
+  if (grp) __builtin_amdgcn_s_barrier();
+#ifdef SAMQ_TUNING
+  // p.dbg & 1: per-wave s_memtime stamps of the four loop segments; & 2: no exp2 (timing only);
+  // & 4: no MFMAs in the MFMA segment (timing only)
+  unsigned long long ph[4] = {0, 0, 0, 0}, tprev = 0;
+  auto stamp = [&](int k) {
+    if (!(p.dbg & 1)) return;
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (tprev) ph[k] += t - tprev;
+    tprev = t;
+  };
+#else
+  auto stamp = [&](int) {};
+#endif
+  for (int kh = 0; kh < S; ++kh) {
+    stamp(3);
+    softmax(kh);
+    if (kh + 1 < S) kread(smem + ((kh + 1) % NSLOT) * ROWB);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pb[0][0]), "+v"(pb[0][1]), "+v"(pb[1][0]), "+v"(pb[1][1]),
+                 "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(kf[0][4]) :: "memory");
+    asm volatile("" : "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]), "+v"(kf[1][4]),
+                 "+v"(o[0]), "+v"(o[1]), "+v"(o[2]) :: "memory");
+    if (grp && kh + 2 < S) retire(kh + 3 < S ? npc : 0);   // row kh+2 (rows kh+3 newer)
+    stamp(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(1);
+    __builtin_amdgcn_s_setprio(1);
+    if (kh + 4 < S) issue(kh + 4, (kh + 4) % NSLOT);
+    pv(kh % NSLOT);
+    if (kh + 1 < S) qk();
+    __builtin_amdgcn_s_setprio(0);
+    if (!grp && kh + 2 < S) retire(npc * ((kh + 3 < S ? 1 : 0) + (kh + 4 < S ? 1 : 0)));   // row kh+2
+    stamp(2);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#ifdef SAMQ_TUNING
+  if ((p.dbg & 1) && lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) atomicAdd(&g_attn_stamps[k + (grp ? 4 : 0)], ph[k]);
+  }
+#endif
+  if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
+
+  // ---- normalise + store: lane = query (qh, qw0 + l32), dims 32 db + 8 c + 4 h .. + 3
+  const float inv = 1.0f / o[2][8];
+  const int64_t dst_tok = (((int64_t)b * p.H + qh) * p.W + qw0 + l32) * C + head * D;
+#pragma unroll
+  for (int db = 0; db < 3; ++db)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (db == 2 && c >= 2) continue;
+      const float4_t v = {o[db][4 * c], o[db][4 * c + 1], o[db][4 * c + 2], o[db][4 * c + 3]};
+      attn_store4(p, dst_tok + 32 * db + 8 * c + 4 * h, v * inv);
+    }
+}
+
+static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
+  AttnParams q = p;
+  q.nqb = 16;
+  q.units = units;
+#ifdef SAMQ_TUNING
+  const char* e = getenv("SAMQ_ATTN_DBG");
+  q.dbg = e ? atoi(e) : 0;
+  if (q.dbg & 1) {
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z));
+  }
+#endif
+  hipLaunchKernelGGL(glob80_attention_kernel, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
+  SAMQ_LAUNCH_CHECK("glob80_attention launch");
+#ifdef SAMQ_TUNING
+  if (q.dbg & 1) {
+    unsigned long long hst[8];
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpyFromSymbol(hst, HIP_SYMBOL(g_attn_stamps), sizeof(hst));
+    const double n = 16.0 * p.heads * units * 4 * 64;   // waves per group x rows
+    fprintf(stderr, "glob80 stamps (cycles per wave-row): grp0 V %.0f bar %.0f M %.0f bar %.0f | grp1 V %.0f bar "
+            "%.0f M %.0f bar %.0f\n", hst[0] / n, hst[1] / n, hst[2] / n, hst[3] / n, hst[4] / n, hst[5] / n,
+            hst[6] / n, hst[7] / n);
+  }
+#endif
+  return SAMQ_OK;
+}
+
 template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
@@ -864,6 +1253,9 @@ static int dispatch_attn(const AttnParams& p, int hd, int units, hipStream_t str
   const int S = p.S;
   if (!PRE && S == 14)   // SAM's window size: two-workgroups-per-CU window kernel
     return hd == 80 ? launch_win<80>(p, units, stream) : launch_win<64>(p, units, stream);
+  // ViT-H global blocks: the 32x32-MFMA kernel (needs heads * units % 8 == 0 for its XCD order)
+  if (!PRE && S == 64 && hd == 80 && (p.heads * units) % 8 == 0 && p.H == 64 && p.W == 64)
+    return launch_glob80(p, units, stream);
   if (S <= 16) {  // whole window / small grid resident in LDS; one query tile per grid row
     if (S == 14)
       return hd == 80 ? launch_attn<80, 16, 2, 7, true, PRE, 14, 14>(p, units, stream)

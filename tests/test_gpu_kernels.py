@@ -240,17 +240,22 @@ def _attn_case(b, h, w, heads, d, window, seed):
     (1, 32, 32, 2, 64, 0),
     (3, 16, 16, 2, 80, 0),
     (2, 14, 14, 2, 80, 0),      # pre-partitioned window as a global 14x14 grid (QuantAttention module path)
+    (2, 64, 64, 4, 80, 0),      # ViT-H global, heads * B % 8 == 0: the 32x32-MFMA kernel
+    (1, 64, 64, 8, 80, 0),
     (1, 64, 64, 1, 80, 0),      # heads * B == 1: the 3-D grid launch (no XCD remap)
     (1, 32, 32, 1, 64, 0),
 ])
 def test_rel_attention(cuda, b, h, w, heads, d, window):
     from samq import ops
     qkv16, bq, rph, rpw, ref = _attn_case(b, h, w, heads, d, window, seed=h * 100 + w + d + window)
-    out = ops.rel_attention(_dev(qkv16, cuda), _dev(bq, cuda), _dev(rph, cuda), _dev(rpw, cuda), heads, window,
-                            d ** -0.5)
+    args = (_dev(qkv16, cuda), _dev(bq, cuda), _dev(rph, cuda), _dev(rpw, cuda), heads, window, d ** -0.5)
+    out = ops.rel_attention(*args)
     torch.cuda.synchronize()
     # fp16 P (2^-11) and fp16 output rounding on |o| <~ 2
     _close(out, ref, 2.5e-3)
+    # deterministic: a second launch is bit-identical (no LDS ring race)
+    for _ in range(3):
+        assert torch.equal(ops.rel_attention(*args), out)
 
 
 @pytest.mark.parametrize("b,h,w,heads,d,window", [
