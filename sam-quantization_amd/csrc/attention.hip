@@ -865,6 +865,9 @@ __device__ __forceinline__ float16_t mfma32(half8_t a, half8_t b, float16_t c) {
 __device__ unsigned long long g_attn_stamps[8];   // timing experiments (tuning build)
 #endif
 
+// DBG (tuning build only): & 1 per-wave s_memtime stamps of the four loop segments; & 2 no exp2,
+// & 4 no MFMAs (timing-only variants, wrong results)
+template <int DBG>
 __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) {
   constexpr int D = 80, S = 64, KS = 5;
   constexpr int NSLOT = 5;                        // key-row ring slots
@@ -872,11 +875,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   constexpr int VB = 10 * 1024;
   constexpr int THB = 64 * 32 * 2;                // per wave: fp16 TH[kh][q]
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 8 * THB];
-#ifdef SAMQ_TUNING
-  const bool DBG_NOEXP = (p.dbg & 2) != 0, DBG_NOMFMA = (p.dbg & 4) != 0;
-#else
-  constexpr bool DBG_NOEXP = false, DBG_NOMFMA = false;
-#endif
+  constexpr bool DBG_NOEXP = (DBG & 2) != 0, DBG_NOMFMA = (DBG & 4) != 0;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
 
@@ -1135,37 +1134,45 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   kread(smem);
   qk();
   if (grp) __builtin_amdgcn_s_barrier();
-#ifdef SAMQ_TUNING
-  // p.dbg & 1: per-wave s_memtime stamps of the four loop segments; & 2: no exp2 (timing only);
-  // & 4: no MFMAs in the MFMA segment (timing only)
   unsigned long long ph[4] = {0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
-    if (!(p.dbg & 1)) return;
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    if (tprev) ph[k] += t - tprev;
-    tprev = t;
+    if constexpr ((DBG & 1) != 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (tprev) ph[k] += t - tprev;
+      tprev = t;
+    }
   };
-#else
-  auto stamp = [&](int) {};
-#endif
-  for (int kh = 0; kh < S; ++kh) {
-    stamp(3);
-    softmax(kh);
-    if (kh + 1 < S) kread(smem + ((kh + 1) % NSLOT) * ROWB);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pb[0][0]), "+v"(pb[0][1]), "+v"(pb[1][0]), "+v"(pb[1][1]),
-                 "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(kf[0][4]) :: "memory");
+  // segment fences: empty volatile asm that "redefines" the registers crossing a barrier, so the
+  // compiler can neither hoist the next row's softmax into the MFMA segment nor sink either
+  // segment's work across its barrier
+  auto fence_sc = [&] {
+    asm volatile("" : "+v"(sc[0]), "+v"(sc[1]), "+v"(o[0]), "+v"(o[1]), "+v"(o[2]) :: "memory");
+  };
+  auto fence_pk = [&] {
+    asm volatile("" : "+v"(pb[0][0]), "+v"(pb[0][1]), "+v"(pb[1][0]), "+v"(pb[1][1]), "+v"(kf[0][0]),
+                 "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(kf[0][4]) :: "memory");
     asm volatile("" : "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]), "+v"(kf[1][4]),
                  "+v"(o[0]), "+v"(o[1]), "+v"(o[2]) :: "memory");
+  };
+  for (int kh = 0; kh < S; ++kh) {
+    stamp(3);
+    fence_sc();
+    softmax(kh);
+    if (kh + 1 < S) kread(smem + ((kh + 1) % NSLOT) * ROWB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    fence_pk();
     if (grp && kh + 2 < S) retire(kh + 3 < S ? npc : 0);   // row kh+2 (rows kh+3 newer)
     stamp(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     stamp(1);
+    fence_pk();
     __builtin_amdgcn_s_setprio(1);
     if (kh + 4 < S) issue(kh + 4, (kh + 4) % NSLOT);
     pv(kh % NSLOT);
     if (kh + 1 < S) qk();
+    fence_sc();
     __builtin_amdgcn_s_setprio(0);
     if (!grp && kh + 2 < S) retire(npc * ((kh + 3 < S ? 1 : 0) + (kh + 4 < S ? 1 : 0)));   // row kh+2
     stamp(2);
@@ -1174,7 +1181,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     __builtin_amdgcn_sched_barrier(0);
   }
 #ifdef SAMQ_TUNING
-  if ((p.dbg & 1) && lane == 0) {
+  if ((DBG & 1) && lane == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) atomicAdd(&g_attn_stamps[k + (grp ? 4 : 0)], ph[k]);
   }
@@ -1206,7 +1213,17 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), z, sizeof(z));
   }
 #endif
-  hipLaunchKernelGGL(glob80_attention_kernel, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
+#ifdef SAMQ_TUNING
+  switch (q.dbg) {
+    case 1: hipLaunchKernelGGL(glob80_attention_kernel<1>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 2: hipLaunchKernelGGL(glob80_attention_kernel<2>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    default: hipLaunchKernelGGL(glob80_attention_kernel<0>, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
+  }
+#else
+  hipLaunchKernelGGL(glob80_attention_kernel<0>, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
+#endif
   SAMQ_LAUNCH_CHECK("glob80_attention launch");
 #ifdef SAMQ_TUNING
   if (q.dbg & 1) {
