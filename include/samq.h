@@ -90,6 +90,31 @@ int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, cons
                         const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M,
                         int N, int K, int groupsize, int epilogue, int cfg, hipStream_t stream);
 
+/* LayerNorm folded into the projection GEMMs around it (the W4A16 encoder block's norm2 between
+ * proj and lin1, and the next block's norm1 between lin2 and qkv; image_encoder.py:194-207):
+ * the HBM round trip of a standalone LayerNorm (read the f32 residual, write the f16 normalised
+ * rows) is replaced by exact algebra,  LN(x).W = rstd*((x - mu_p)*gamma).W - rstd*delta*(gamma.W)
+ * + beta.W,  with mu_p the row mean of the PREVIOUS LayerNorm of the same row (so the f16 operand
+ * (x - mu_p)*gamma carries no large mean) and delta = mean(x) - mu_p from per-row partial sums:
+ *   SAMQ_EPI_RESADD_LNF (producer, C f32 [M,N] residual x += y in place), then
+ *     aout f16 [M,N] = f16((x_new - mu[r]) * gamma[n]) and, per 64-column block b,
+ *     stats[(r*(N/64) + b)*2 + {0,1}] = sum over the block of (x_new - mu[r]), (x_new - mu[r])^2;
+ *   SAMQ_EPI_BIAS_LNF / SAMQ_EPI_GELU_LNF (consumer, A = the producer's aout, K = its N):
+ *     delta = S1/K, rstd = 1/sqrt(S2/K - delta^2 + eps) from stats[r, 0..K/64),
+ *     C f16 = y = rstd*(acc*scale[n] - delta*gw[n]) + bw[n] + bias[n]  (GELU_erf(y) for GELU_LNF),
+ *     gw = gamma.W, bw = beta.W (f32 [N], the next LayerNorm's weights times this layer's dequantised
+ *     weight); the tiles of column block 0 set mu[r] += delta (the next producer's mu_p). */
+#define SAMQ_EPI_RESADD_LNF 7
+#define SAMQ_EPI_BIAS_LNF 8
+#define SAMQ_EPI_GELU_LNF 9
+/* samq_w4a16_gemm_cfg with the LayerNorm-fold epilogues above (ping-pong configs 57 / 64 / 0 =
+ * automatic at M >= 8192 only, else SAMQ_ERR_UNSUPPORTED): gamma f32 [N] (producer), gw / bw f32
+ * [N] (consumer), stats f32, mu f32 [M], aout f16 [M,N] (producer), eps of the folded LayerNorm. */
+int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                        const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N, int K,
+                        int groupsize, int epilogue, int cfg, const float* gamma, const float* gw,
+                        const float* bw, float* stats, float* mu, void* aout, float eps, hipStream_t stream);
+
 /* ---------------------------------------------------------------- int8 activations */
 
 /* fq_vit int8 weights: W int8 [N][K] row-major (QLinear / flattened QConv2d weight codes,
@@ -180,6 +205,10 @@ int samq_silu_mul(const float* gate, const float* up, void* out, int64_t n, hipS
 #define SAMQ_LN_RPW(n) ((n) << 16)
 int samq_layernorm(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
                    int C, float eps, int flags, hipStream_t stream);
+/* samq_layernorm that also writes the row means (f32 [rows]) -- the mu_p of the first folded
+ * LayerNorm (SAMQ_EPI_RESADD_LNF) downstream. */
+int samq_layernorm_mean(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                        int C, float eps, int flags, float* mean_out, hipStream_t stream);
 
 /* LayerNorm with int8 activation codes on either side (fq_vit QIntLayerNorm = nn.LayerNorm
  * between two QActs, layers.py:245-258, fq_vit/models/sam/image_encoder.py:310-331; neck

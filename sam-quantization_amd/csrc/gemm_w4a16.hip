@@ -339,6 +339,88 @@ __device__ __forceinline__ half8_t scale8(half8_t v, half2_t s) {
   return v;
 }
 
+// ---- LayerNorm-fold epilogues (SAMQ_EPI_RESADD_LNF / BIAS_LNF / GELU_LNF, include/samq.h)
+struct LnfArgs {
+  const float* gamma;   // producer: the next LayerNorm's weight [N]
+  const float* gw;      // consumer: gamma . W [N]
+  const float* bw;      // consumer: beta . W [N]
+  float* stats;         // [M][N_producer / 64][2] partial sums of (x - mu_p), (x - mu_p)^2
+  float* mu;            // [M] row mean of the previous LayerNorm (consumer: += delta)
+  _Float16* aout;       // producer: f16 (x - mu_p) * gamma [M][N]
+  float eps;
+  int nblk;             // consumer: K / 64 partial-sum blocks per row
+  const _Float16* bias; // consumer: the layer bias (set by the kernel)
+};
+constexpr bool lnf_producer(int epi) { return epi == SAMQ_EPI_RESADD_LNF; }
+constexpr bool lnf_consumer(int epi) { return epi == SAMQ_EPI_BIAS_LNF || epi == SAMQ_EPI_GELU_LNF; }
+constexpr bool epi_f32_out(int epi) {
+  return epi == SAMQ_EPI_RESADD_F32 || epi == SAMQ_EPI_F32 || epi == SAMQ_EPI_RESADD_LNF;
+}
+
+// producer: one f32 residual row chunk (4 columns at col of row) x_new = x + v, its f16 fold
+// operand and this lane's partial sums; the caller reduces the sums over the 16 lanes of a row
+__device__ __forceinline__ void lnf_res4(const LnfArgs& L, float* C, int64_t ldc, int N, int64_t row, int col,
+                                         float4_t v, float& s1, float& s2) {
+  float4_t* cp = (float4_t*)(C + row * ldc + col);
+  const float4_t x = *cp + v;
+  *cp = x;
+  const float m = L.mu[row];
+  const float4_t g = *(const float4_t*)(L.gamma + col);
+  const float4_t d = x - m;
+  *(half4_t*)(L.aout + row * N + col) = half4_t{(_Float16)(d[0] * g[0]), (_Float16)(d[1] * g[1]),
+                                                (_Float16)(d[2] * g[2]), (_Float16)(d[3] * g[3])};
+  s1 = (d[0] + d[1]) + (d[2] + d[3]);
+  s2 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+}
+// ... reduced over 16 lanes (xor 1, 2, 4, 8: one row), lane 0 of the 16 writes the block's pair
+__device__ __forceinline__ void lnf_stats16(const LnfArgs& L, int N, int64_t row, int col_block, bool valid,
+                                            float s1, float s2, int c4) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (valid && c4 == 0) *(float2_t*)(L.stats + (row * (N / 64) + col_block) * 2) = float2_t{s1, s2};
+}
+// consumer: (delta, rstd) of the wave's WM rows into LDS (rowinfo), mu += delta by column block 0
+template <int WM>
+__device__ __forceinline__ void lnf_rowinfo(const LnfArgs& L, float2_t* rowinfo, int M, int row_base, bool col0,
+                                            int lane) {
+  const float inv_k = 1.0f / (float)(L.nblk * 64);
+#pragma unroll
+  for (int q = 0; q < WM / 64; ++q) {
+    const int rl = q * 64 + lane;
+    const int64_t row = row_base + rl;
+    float s1 = 0.f, s2 = 0.f;
+    if (row < M) {
+      const float2_t* sp = (const float2_t*)(L.stats + row * L.nblk * 2);
+      for (int b = 0; b < L.nblk; ++b) {
+        const float2_t v = sp[b];
+        s1 += v.x;
+        s2 += v.y;
+      }
+    }
+    const float delta = s1 * inv_k;
+    const float var = fmaxf(s2 * inv_k - delta * delta, 0.0f);
+    rowinfo[rl] = float2_t{delta, rsqrtf(var + L.eps)};
+    if (col0 && row < M) L.mu[row] += delta;
+  }
+}
+// consumer store of 8 columns: y = rstd * (v - delta * gw) + (bw + bias) (-> GELU), f16
+template <int EPI>
+__device__ __forceinline__ half8_t lnf_out8(float4_t v0, float4_t v1, float2_t ri, const float (&gw)[8],
+                                           const float (&bb)[8]) {
+  float y[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  half8_t h;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float t = __builtin_fmaf(ri.y, __builtin_fmaf(-ri.x, gw[e], y[e]), bb[e]);
+    if (EPI == SAMQ_EPI_GELU_LNF) t = gelu_fast(t);
+    h[e] = (_Float16)t;
+  }
+  return h;
+}
+
 // The same epilogue for 16x16x32 accumulators (VAR & 16 of the ping-pong kernel): lane (ql, g)
 // of 16-row tile i, 32-column block t, half h holds rows 16i + 4g + r of column 32t + 16h + ql;
 // staged per 16-row tile with a padded pitch (WN + 4 floats: the four lane groups' rows land
@@ -346,10 +428,22 @@ __device__ __forceinline__ half8_t scale8(half8_t v, half2_t s) {
 template <int TM16, int TN, int EPI>
 __device__ __forceinline__ void pp_epilogue16(const float4_t (&acc)[TM16][TN][2], const float (&csc)[TN][2],
                                               const float (&cb)[TN][2], char* ep_bytes, void* Cout, int64_t ldc,
-                                              int M, int row_base, int col_base, int lane) {
+                                              int M, int row_base, int col_base, int lane,
+                                              const LnfArgs& L = LnfArgs{}, int N = 0,
+                                              const float2_t* rowinfo = nullptr) {
   constexpr int WN = TN * 32, EP_ROWS = 16, PITCH = WN + 4;
+  static_assert(!(lnf_producer(EPI) || lnf_consumer(EPI)) || WN == 64, "LN fold: 64-column wave tiles");
   float* ep = (float*)ep_bytes;
   const int ql = lane & 15, g = lane >> 4;
+  float gw8[8], bb8[8];   // LNF consumer: this lane's 8 columns (fixed over the slices)
+  if constexpr (lnf_consumer(EPI)) {
+    const int c0 = col_base + 8 * (lane % (WN / 8));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gw8[e] = L.gw[c0 + e];
+      bb8[e] = L.bw[c0 + e] + (L.bias ? (float)L.bias[c0 + e] : 0.0f);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM16; ++i) {
 #pragma unroll
@@ -358,13 +452,26 @@ __device__ __forceinline__ void pp_epilogue16(const float4_t (&acc)[TM16][TN][2]
       for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float v = acc[i][t][h][r] * csc[t][h] + cb[t][h];
+          float v = lnf_consumer(EPI) ? acc[i][t][h][r] * csc[t][h] : acc[i][t][h][r] * csc[t][h] + cb[t][h];
           if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast(v);
           ep[(4 * g + r) * PITCH + 32 * t + 16 * h + ql] = v;
         }
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
     const int srow0 = row_base + i * 16;
-    if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+    if (lnf_producer(EPI)) {
+      constexpr int C4 = WN / 4;
+      static_assert((EP_ROWS * C4) % 64 == 0, "LN fold: whole waves per slice");
+#pragma unroll
+      for (int j = 0; j < EP_ROWS * C4 / 64; ++j) {
+        const int idx = j * 64 + lane;
+        const int rl = idx / C4, c4 = idx % C4;
+        const int row = srow0 + rl;
+        const float4_t v = *(const float4_t*)(ep + rl * PITCH + 4 * c4);
+        float s1 = 0.f, s2 = 0.f;
+        if (row < M) lnf_res4(L, (float*)Cout, ldc, N, row, col_base + 4 * c4, v, s1, s2);
+        lnf_stats16(L, N, row, col_base / 64, row < M, s1, s2, c4);
+      }
+    } else if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
       constexpr int C4 = WN / 4;
 #pragma unroll
       for (int j = 0; j < (EP_ROWS * C4 + 63) / 64; ++j) {
@@ -376,6 +483,22 @@ __device__ __forceinline__ void pp_epilogue16(const float4_t (&acc)[TM16][TN][2]
           if (row < M) {
             float4_t* cp = (float4_t*)((float*)Cout + (int64_t)row * ldc + col_base + 4 * c4);
             if (EPI == SAMQ_EPI_RESADD_F32) *cp = *cp + v; else *cp = v;
+          }
+        }
+      }
+    } else if (lnf_consumer(EPI)) {
+      constexpr int C8 = WN / 8;
+#pragma unroll
+      for (int j = 0; j < (EP_ROWS * C8 + 63) / 64; ++j) {
+        const int idx = j * 64 + lane;
+        if (idx < EP_ROWS * C8) {
+          const int rl = idx / C8, c8 = idx % C8;
+          const int row = srow0 + rl;
+          const float4_t v0 = *(const float4_t*)(ep + rl * PITCH + 8 * c8);
+          const float4_t v1 = *(const float4_t*)(ep + rl * PITCH + 8 * c8 + 4);
+          if (row < M) {
+            const float2_t ri = rowinfo[row - row_base];
+            *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = lnf_out8<EPI>(v0, v1, ri, gw8, bb8);
           }
         }
       }
@@ -811,11 +934,23 @@ void w4a16_gemm_v4(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
 template <int TM, int TN, int EP_ROWS, int EPI>
 __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], const float (&csc)[TN],
                                             const float (&cb)[TN], char* ep_bytes, void* Cout, int64_t ldc,
-                                            int M, int row_base, int col_base, int lane) {
+                                            int M, int row_base, int col_base, int lane,
+                                            const LnfArgs& L = LnfArgs{}, int N = 0,
+                                            const float2_t* rowinfo = nullptr) {
   constexpr int WN = TN * 32;
   constexpr int NSL = 32 / EP_ROWS;
+  static_assert(!(lnf_producer(EPI) || lnf_consumer(EPI)) || WN == 64, "LN fold: 64-column wave tiles");
   float* ep = (float*)ep_bytes;
   const int hsel = lane >> 5;
+  float gw8[8], bb8[8];   // LNF consumer: this lane's 8 columns (fixed over the slices)
+  if constexpr (lnf_consumer(EPI)) {
+    const int c0 = col_base + 8 * (lane % (WN / 8));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      gw8[e] = L.gw[c0 + e];
+      bb8[e] = L.bw[c0 + e] + (L.bias ? (float)L.bias[c0 + e] : 0.0f);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -827,7 +962,7 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
 #pragma unroll
         for (int t = 0; t < TN; ++t) {
           float2_t v = __builtin_elementwise_fma((float2_t){acc[i][t][r], acc[i][t][r + 1]}, (float2_t)(csc[t]),
-                                                 (float2_t)(cb[t]));
+                                                 (float2_t)(lnf_consumer(EPI) ? 0.0f : cb[t]));
           if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast2(v);
           ep[rl * WN + t * 32 + (lane & 31)] = v.x;
           ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
@@ -835,7 +970,36 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
       const int srow0 = row_base + i * 32 + sl * EP_ROWS;
-      if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
+      if (lnf_producer(EPI)) {
+        constexpr int C4 = WN / 4;
+        static_assert((EP_ROWS * C4) % 64 == 0, "LN fold: whole waves per slice");
+#pragma unroll
+        for (int j = 0; j < EP_ROWS * C4 / 64; ++j) {
+          const int idx = j * 64 + lane;
+          const int rl = idx / C4, c4 = idx % C4;
+          const int row = srow0 + rl;
+          const float4_t v = ((const float4_t*)ep)[idx];
+          float s1 = 0.f, s2 = 0.f;
+          if (row < M) lnf_res4(L, (float*)Cout, ldc, N, row, col_base + 4 * c4, v, s1, s2);
+          lnf_stats16(L, N, row, col_base / 64, row < M, s1, s2, c4);
+        }
+      } else if (lnf_consumer(EPI)) {
+        constexpr int C8 = WN / 8;
+#pragma unroll
+        for (int j = 0; j < (EP_ROWS * C8 + 63) / 64; ++j) {
+          const int idx = j * 64 + lane;
+          if (idx < EP_ROWS * C8) {
+            const int rl = idx / C8, c8 = idx % C8;
+            const int row = srow0 + rl;
+            const float4_t v0 = ((const float4_t*)ep)[2 * idx];
+            const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+            if (row < M) {
+              const float2_t ri = rowinfo[row - row_base];
+              *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = lnf_out8<EPI>(v0, v1, ri, gw8, bb8);
+            }
+          }
+        }
+      } else if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
         constexpr int C4 = WN / 4;
 #pragma unroll
         for (int j = 0; j < (EP_ROWS * C4 + 63) / 64; ++j) {
@@ -945,7 +1109,7 @@ __global__ __launch_bounds__(512, 1)
 void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
                     const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
                     const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
-                    int M, int N, int K, int kpg) {
+                    int M, int N, int K, int kpg, LnfArgs lnf) {
   constexpr int NW = 8;
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = TM * 32, WN = TN * 32;
@@ -991,7 +1155,9 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   constexpr int KS32 = 2 / NPH;                  // M16: k32 steps per phase
   constexpr int EP_ROWS = WN > 64 ? 16 : 32;
   constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : EP_ROWS * WN * 4;
-  constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES ? STAGES * STAGE : NW * EP_BYTES;
+  // LN-fold consumers: per-wave (delta, rstd) of its WM rows behind the epilogue slices
+  constexpr int RI_BYTES = lnf_consumer(EPI) ? NW * WM * 8 : 0;
+  constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES + RI_BYTES ? STAGES * STAGE : NW * EP_BYTES + RI_BYTES;
   static_assert(!M16 || NPH <= 2, "M16: one or two phases per K tile");
   static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
   static_assert(LA >= 2 && LA < STAGES, "ring");
@@ -1354,8 +1520,14 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
         cb16[t][h] = bias ? (float)bias[c] : 0.0f;
       }
     __syncthreads();
+    float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES + wave * WM * 8);
+    lnf.bias = bias;
+    if constexpr (lnf_consumer(EPI)) {
+      lnf_rowinfo<WM>(lnf, rowinfo, M, m0 + wm * WM, n0 + wn * WN == 0, lane);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
     pp_epilogue16<2 * TM, TN, EPI>(acc16, csc16, cb16, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
-                                   n0 + wn * WN, lane);
+                                   n0 + wn * WN, lane, lnf, N, rowinfo);
     return;
   }
   float csc[TN], cb[TN];
@@ -1365,14 +1537,21 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     cb[t] = bias ? (float)bias[col[t]] : 0.0f;
   }
   __syncthreads();
+  float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES + wave * WM * 8);
+  lnf.bias = bias;
+  if constexpr (lnf_consumer(EPI)) {
+    lnf_rowinfo<WM>(lnf, rowinfo, M, m0 + wm * WM, n0 + wn * WN == 0, lane);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
   pp_epilogue<TM, TN, EP_ROWS, EPI>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
-                                    n0 + wn * WN, lane);
+                                    n0 + wn * WN, lane, lnf, N, rowinfo);
 }
 
 // ------------------------------------------------------------------ dispatch
 struct GemmArgs {
   const _Float16* A; int64_t lda; const u32x4* Wp; const _Float16* scales; const uint32_t* qzeros;
   const _Float16* bias; void* C; int64_t ldc; int M, N, K, groupsize;
+  LnfArgs lnf;
 };
 
 template <int BM, int BN, int WMW, int WNW, int EPI, bool GR, int VAR = 1>
@@ -1407,9 +1586,22 @@ static int launch_pp2(const GemmArgs& a, hipStream_t st) {
   constexpr int BM = WMW * TM * 32, BN = (8 / WMW) * TN * 32;
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
-                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64);
+                     a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64, a.lnf);
   SAMQ_LAUNCH_CHECK("w4a16_gemm_pp2 launch");
   return SAMQ_OK;
+}
+
+// LayerNorm-fold epilogues: the product ping-pong configs only
+template <int EPI, bool GR>
+static int launch_lnf(const GemmArgs& a, int cfg, hipStream_t st) {
+  if (GR) {
+    if (cfg == 57) return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
+    if (cfg == 64) return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16>(a, st);
+  } else {
+    if (cfg == 57) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
+    if (cfg == 64) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);
+  }
+  return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm_lnf: the LayerNorm fold needs ping-pong config 57 or 64");
 }
 
 template <int EPI, bool GR>
@@ -1643,6 +1835,42 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
     case SAMQ_EPI_RESADD_F32: return gr ? launch_epi<SAMQ_EPI_RESADD_F32, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_RESADD_F32, false>(a, cfg, stream);
     case SAMQ_EPI_F32: return gr ? launch_epi<SAMQ_EPI_F32, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_F32, false>(a, cfg, stream);
     default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown epilogue");
+  }
+}
+
+extern "C" int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                                   const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N,
+                                   int K, int groupsize, int epilogue, int cfg, const float* gamma, const float* gw,
+                                   const float* bw, float* stats, float* mu, void* aout, float eps,
+                                   hipStream_t stream) {
+  SAMQ_REQUIRE(A && wpacked && scales && qzeros && C && stats && mu, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: null pointer");
+  SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0 && N % 256 == 0, SAMQ_ERR_INVALID,
+               "w4a16_gemm_lnf: K % 64 == 0 and N % 256 == 0 required");
+  SAMQ_REQUIRE(lda >= K && lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ldc >= N && ldc % 8 == 0 &&
+               ((uintptr_t)C & 15) == 0, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: 16-byte aligned A / C rows required");
+  if (groupsize == -1) groupsize = K;
+  SAMQ_REQUIRE(groupsize > 0 && (groupsize == K || groupsize % 64 == 0), SAMQ_ERR_INVALID,
+               "w4a16_gemm_lnf: groupsize must be -1, K, or a multiple of 64");
+  const bool gr = groupsize != K;
+  if (cfg <= 0) cfg = pick_cfg(M, N, gr);
+  LnfArgs L{gamma, gw, bw, stats, mu, (_Float16*)aout, eps, K / 64, nullptr};
+  if (epilogue == SAMQ_EPI_RESADD_LNF) {
+    SAMQ_REQUIRE(gamma && aout, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: the producer needs gamma and aout");
+  } else if (epilogue == SAMQ_EPI_BIAS_LNF || epilogue == SAMQ_EPI_GELU_LNF) {
+    SAMQ_REQUIRE(gw && bw, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: the consumer needs gw and bw");
+  } else {
+    return fail(SAMQ_ERR_INVALID, "w4a16_gemm_lnf: epilogue must be RESADD_LNF, BIAS_LNF or GELU_LNF");
+  }
+  if (M == 0) return SAMQ_OK;
+  GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
+             (const _Float16*)bias, C, ldc, M, N, K, groupsize, L};
+  switch (epilogue) {
+    case SAMQ_EPI_RESADD_LNF: return gr ? launch_lnf<SAMQ_EPI_RESADD_LNF, true>(a, cfg, stream)
+                                        : launch_lnf<SAMQ_EPI_RESADD_LNF, false>(a, cfg, stream);
+    case SAMQ_EPI_BIAS_LNF: return gr ? launch_lnf<SAMQ_EPI_BIAS_LNF, true>(a, cfg, stream)
+                                      : launch_lnf<SAMQ_EPI_BIAS_LNF, false>(a, cfg, stream);
+    default: return gr ? launch_lnf<SAMQ_EPI_GELU_LNF, true>(a, cfg, stream)
+                       : launch_lnf<SAMQ_EPI_GELU_LNF, false>(a, cfg, stream);
   }
 }
 

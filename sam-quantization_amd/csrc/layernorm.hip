@@ -18,7 +18,8 @@ template <int IN, int OUT, int VPT, int RPW>  // VPT = 4-channel vectors per lan
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ xin, void* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows, int C,
-                                                        float eps, float in_scale, float out_scale) {
+                                                        float eps, float in_scale, float out_scale,
+                                                        float* __restrict__ mean_out) {
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= rows) return;
@@ -55,6 +56,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 #pragma unroll
     for (int i = 0; i < VPT; ++i) s += v[r][i][0] + v[r][i][1] + v[r][i][2] + v[r][i][3];
     const float mean = wave_sum(s) / (float)C;
+    if (mean_out && lane == 0) mean_out[row] = mean;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
@@ -108,7 +110,8 @@ static int ln_rpw(int flags) {
 }
 
 static int ln_launch(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C, float eps,
-                     int in, int out, float in_scale, float out_scale, int rpw, hipStream_t stream) {
+                     int in, int out, float in_scale, float out_scale, int rpw, hipStream_t stream,
+                     float* mean_out = nullptr) {
   SAMQ_REQUIRE(x && y && gamma && beta, SAMQ_ERR_INVALID, "layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 4096, SAMQ_ERR_INVALID, "layernorm: C must be a multiple of 4, <= 4096");
   if (rows <= 0) return SAMQ_OK;
@@ -118,9 +121,9 @@ static int ln_launch(const void* x, void* y, const float* gamma, const float* be
   const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
 #define LN_R(I, O, V) \
   do { \
-    if (rpw == 1) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 2>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
-    else hipLaunchKernelGGL((layernorm_kernel<I, O, V, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale); \
+    if (rpw == 1) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
+    else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 2>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
+    else hipLaunchKernelGGL((layernorm_kernel<I, O, V, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
   } while (0)
 #define LN_V(I, O) \
   do { \
@@ -147,6 +150,13 @@ extern "C" int samq_layernorm(const void* x, void* y, const float* gamma, const 
                               float eps, int flags, hipStream_t stream) {
   return ln_launch(x, y, gamma, beta, rows, C, eps, (flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32,
                    (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, ln_rpw(flags), stream);
+}
+
+extern "C" int samq_layernorm_mean(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                                   int C, float eps, int flags, float* mean_out, hipStream_t stream) {
+  SAMQ_REQUIRE(mean_out, SAMQ_ERR_INVALID, "layernorm_mean: null mean_out");
+  return ln_launch(x, y, gamma, beta, rows, C, eps, (flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32,
+                   (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, ln_rpw(flags), stream, mean_out);
 }
 
 extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,

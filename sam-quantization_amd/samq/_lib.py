@@ -28,6 +28,9 @@ EPI_F32 = 3
 EPI_Q8 = 4
 EPI_Q8_GELU = 5
 EPI_Q8_RES = 6
+EPI_RESADD_LNF = 7
+EPI_BIAS_LNF = 8
+EPI_GELU_LNF = 9
 
 BF_W8 = 0
 BF_W4 = 1
@@ -57,6 +60,8 @@ SIGNATURES = {
     "samq_w4_repack_layout": (_i32, [_vp, _vp, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_w4a16_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _vp]),
+    "samq_w4a16_gemm_lnf": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _i32,
+                                   _vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp]),
     "samq_w8_repack": (_i32, [_vp, _vp, _i32, _i32, _vp]),
     "samq_w8a8_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _i32,
                               _f32, _f32, _f32, _f32, _vp]),
@@ -71,6 +76,7 @@ SIGNATURES = {
     "samq_minmax": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, ctypes.c_size_t, _vp]),
     "samq_silu_mul": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
+    "samq_layernorm_mean": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp]),
     "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),
     "samq_rel_attention": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp]),
     "samq_rel_attention_q": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _f32, _vp]),

@@ -35,7 +35,8 @@ from .quant_linear import QuantLinear
 
 class _BlockPlan:
     __slots__ = ("ln1_w", "ln1_b", "ln1_eps", "qkv", "proj", "relh", "relw", "heads", "window", "scale",
-                 "ln2_w", "ln2_b", "ln2_eps", "lin1", "lin2", "qkv_bias", "s_qkv", "s_proj", "s_lin1", "s_lin2")
+                 "ln2_w", "ln2_b", "ln2_eps", "lin1", "lin2", "qkv_bias", "s_qkv", "s_proj", "s_lin1", "s_lin2",
+                 "qkv_gw", "qkv_bw", "lin1_gw", "lin1_bw")
 
 
 class EncoderEngine:
@@ -46,6 +47,9 @@ class EncoderEngine:
         self.C = enc.embed_dim
         self.grid = enc.img_size // enc.patch_size
         self.ln_rpw = 0   # LayerNorm rows per wave (0 = library default; in-graph A/B knob)
+        # fold norm2 / the next block's norm1 into the GEMMs around them (W4A16, >= 8192 rows per
+        # chain: the ping-pong GEMMs carry the fold epilogues); False = standalone LayerNorms
+        self.fold_ln = True
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
@@ -80,6 +84,7 @@ class EncoderEngine:
             for p in self.plans:
                 for lin in (p.qkv, p.proj, p.lin1, p.lin2):
                     lin.prepare_w4a8()
+        self._fold_ready = False
         pe = enc.patch_embed.proj
         self.patch = pe.kernel_size[0]
         self.pe_w = pe.weight.detach().reshape(pe.weight.shape[0], -1).to(torch.float16).contiguous()
@@ -146,6 +151,9 @@ class EncoderEngine:
                 att=torch.empty((b, g, g, c), dtype=torch.float16, device=dev),
                 hid=torch.empty((b, g, g, hid), dtype=torch.float16, device=dev),
             )
+            if not self.w4a8:   # LayerNorm fold: per-row partial sums (64-column blocks) and means
+                bufs.update(stats=torch.empty((b * g * g, c // 64, 2), dtype=torch.float32, device=dev),
+                            mu=torch.empty((b * g * g,), dtype=torch.float32, device=dev))
             if self.w4a8:
                 bufs.update(xn8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
                             att8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
@@ -190,6 +198,47 @@ class EncoderEngine:
         p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
         p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
 
+    # ---------------------------------------------------------------- LayerNorm fold
+    def _fold_usable(self, rows: int) -> bool:
+        """The fold epilogues live in the ping-pong GEMMs (configs 57 / 64), which the library picks
+        from 8192 rows up; every block Linear must use that pick (gemm_cfg 0, 57 or 64)."""
+        if self.w4a8 or not self.fold_ln or rows < 8192 or self.C % 256:
+            return False
+        return all(lin.gemm_cfg in (0, 57, 64) and lin.outfeatures % 256 == 0
+                   for p in self.plans for lin in (p.qkv, p.proj, p.lin1, p.lin2))
+
+    def _prepare_fold(self) -> None:
+        """gamma . W and beta . W of every folded LayerNorm's consumer (norm1 -> qkv for blocks >= 1,
+        norm2 -> lin1), from the layers' own GEMMs -- once per engine."""
+        if self._fold_ready:
+            return
+        for p in self.plans:
+            p.qkv_gw, p.qkv_bw = p.qkv.ln_fold_constants(p.ln1_w, p.ln1_b)
+            p.lin1_gw, p.lin1_bw = p.lin1.ln_fold_constants(p.ln2_w, p.ln2_b)
+        self._fold_ready = True
+
+    def block_fold(self, i: int, bufs) -> None:
+        """W4A16 block with the LayerNorms folded into the GEMMs (samq_w4a16_gemm_lnf, include/samq.h):
+        proj's residual epilogue emits f16((x - mu) * gamma2) + per-row partial sums, lin1's
+        epilogue applies LN2 algebraically (rstd * (acc - delta * gamma2.W1) + beta2.W1 + b1, GELU);
+        lin2's residual epilogue does the same for the next block's norm1 and its qkv consumes it.
+        Block 0's norm1 stays a LayerNorm kernel (it also writes the row means mu)."""
+        p = self.plans[i]
+        x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
+        st, mu = bufs["stats"], bufs["mu"]
+        if i == 0:
+            ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw, mean_out=mu)
+            p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
+        else:
+            p.qkv.forward_lnf(xn, ops.EPI_BIAS_LNF, qkv, st, mu, gw=p.qkv_gw, bw=p.qkv_bw, eps=p.ln1_eps)
+        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        p.proj.forward_lnf(att, ops.EPI_RESADD_LNF, x, st, mu, gamma=p.ln2_w, aout=xn)
+        p.lin1.forward_lnf(xn, ops.EPI_GELU_LNF, hid, st, mu, gw=p.lin1_gw, bw=p.lin1_bw, eps=p.ln2_eps)
+        if i + 1 < len(self.plans):
+            p.lin2.forward_lnf(hid, ops.EPI_RESADD_LNF, x, st, mu, gamma=self.plans[i + 1].ln1_w, aout=xn)
+        else:
+            p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
+
     def block(self, p: _BlockPlan, bufs) -> None:
         if self.w4a8:
             return self.block_w4a8(p, bufs)
@@ -233,6 +282,9 @@ class EncoderEngine:
             out_dtype = out_dtype or torch.float32
         out_dtype = out_dtype or img.dtype
         b = img.shape[0]
+        per_chain = b // min(max(lanes, 1), b) if lanes > 1 and b >= 2 else b
+        if self._fold_usable(per_chain * self.grid * self.grid):
+            self._prepare_fold()   # on the current stream, before any lane fork
         if lanes <= 1 or b < 2:
             return self._forward(img, self.buffers(b), out_dtype)
         lanes = min(lanes, b)
@@ -263,8 +315,12 @@ class EncoderEngine:
 
     def _forward(self, img: torch.Tensor, bufs, out_dtype) -> torch.Tensor:
         self.embed(img, bufs["x"])
-        for p in self.plans:
-            self.block(p, bufs)
+        if self._fold_ready and self._fold_usable(bufs["x"].numel() // self.C):
+            for i in range(len(self.plans)):
+                self.block_fold(i, bufs)
+        else:
+            for p in self.plans:
+                self.block(p, bufs)
         return self.neck(bufs["x"], out_dtype)
 
     __call__ = forward

@@ -18,6 +18,9 @@ EPI_F32 = _lib.EPI_F32
 EPI_Q8 = _lib.EPI_Q8
 EPI_Q8_GELU = _lib.EPI_Q8_GELU
 EPI_Q8_RES = _lib.EPI_Q8_RES
+EPI_RESADD_LNF = _lib.EPI_RESADD_LNF
+EPI_BIAS_LNF = _lib.EPI_BIAS_LNF
+EPI_GELU_LNF = _lib.EPI_GELU_LNF
 
 # W4A16 tile configs of the product library (include/samq.h, samq_w4a16_gemm_cfg); 0 = automatic
 W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65))
@@ -81,10 +84,36 @@ def w4a16_gemm(a: torch.Tensor, wpacked: torch.Tensor, scales: torch.Tensor, qze
     return out
 
 
+def w4a16_gemm_lnf(a: torch.Tensor, wpacked: torch.Tensor, scales: torch.Tensor, qzeros: torch.Tensor,
+                   bias: Optional[torch.Tensor], n: int, groupsize: int, epilogue: int, out: torch.Tensor,
+                   stats: torch.Tensor, mu: torch.Tensor, gamma: Optional[torch.Tensor] = None,
+                   aout: Optional[torch.Tensor] = None, gw: Optional[torch.Tensor] = None,
+                   bw: Optional[torch.Tensor] = None, eps: float = 1e-6, cfg: int = 0) -> torch.Tensor:
+    """The W4A16 GEMM with a LayerNorm folded into its epilogue (samq_w4a16_gemm_lnf,
+    include/samq.h): ``EPI_RESADD_LNF`` -- out f32 residual += y, then aout = f16((x - mu) * gamma)
+    and the per-row partial sums ``stats``; ``EPI_BIAS_LNF`` / ``EPI_GELU_LNF`` -- out f16 =
+    LN(x) . W + bias (GELU) from a = that aout, ``stats`` and gw = gamma . W, bw = beta . W; mu += delta."""
+    _need_cuda(a, wpacked, scales, qzeros, bias, out, stats, mu, gamma, aout, gw, bw)
+    assert a.dtype == torch.float16 and a.is_contiguous() and out.is_contiguous()
+    k = a.shape[-1]
+    m = a.numel() // k
+    assert out.numel() == m * n and stats.dtype == torch.float32 and mu.dtype == torch.float32 and mu.numel() >= m
+    if epilogue == EPI_RESADD_LNF:
+        assert out.dtype == torch.float32 and gamma is not None and aout is not None and aout.numel() == m * n
+        assert stats.numel() >= m * (n // 64) * 2
+    else:
+        assert out.dtype == torch.float16 and gw is not None and bw is not None and stats.numel() >= m * (k // 64) * 2
+    status = _lib.load().samq_w4a16_gemm_lnf(
+        _ptr(a), k, _ptr(wpacked), _ptr(scales), _ptr(qzeros), _ptr(bias), _ptr(out), n, m, n, k, groupsize,
+        epilogue, cfg, _ptr(gamma), _ptr(gw), _ptr(bw), _ptr(stats), _ptr(mu), _ptr(aout), float(eps), _stream())
+    _lib.check(status, "w4a16_gemm_lnf")
+    return out
+
+
 # ----------------------------------------------------------------------------- LayerNorm
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-6,
               out: Optional[torch.Tensor] = None, out_dtype: torch.dtype = torch.float16,
-              rows_per_wave: int = 0) -> torch.Tensor:
+              rows_per_wave: int = 0, mean_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row LayerNorm over the last dim; x f32 or f16 -> f16 (or f32); gamma/beta f32.
     ``rows_per_wave`` (1, 2, 4; 0 = library default) is a tuning knob (SAMQ_LN_RPW)."""
     _need_cuda(x, gamma, beta)
@@ -97,6 +126,11 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     flags = (_lib.LN_IN_F16 if x.dtype == torch.float16 else 0) | (_lib.LN_OUT_F32 if out.dtype == torch.float32 else 0)
     flags |= rows_per_wave << 16
     rows = x.numel() // c
+    if mean_out is not None:
+        assert mean_out.dtype == torch.float32 and mean_out.numel() >= rows and mean_out.is_cuda
+        _lib.check(_lib.load().samq_layernorm_mean(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), rows, c, float(eps),
+                                                   flags, _ptr(mean_out), _stream()), "layernorm_mean")
+        return out
     _lib.check(_lib.load().samq_layernorm(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), rows, c, float(eps), flags,
                                           _stream()), "layernorm")
     return out

@@ -116,6 +116,27 @@ class QuantLinear(nn.Module):
         return ops.w4a8_gemm(codes, w["packed"], w["scale"], self.qzeros, self.outfeatures, w["bias"], epilogue,
                              a_scale, out_scale, out=out, cfg=getattr(self, "i8_cfg", 0))
 
+    def forward_lnf(self, x: torch.Tensor, epilogue: int, out: torch.Tensor, stats: torch.Tensor, mu: torch.Tensor,
+                    **kw) -> torch.Tensor:
+        """The W4A16 GEMM with a LayerNorm folded into its epilogue (ops.w4a16_gemm_lnf)."""
+        return ops.w4a16_gemm_lnf(x, self.prepare(), self.scales, self.qzeros, self.bias, self.outfeatures,
+                                  self.groupsize, epilogue, out, stats, mu, cfg=self.gemm_cfg, **kw)
+
+    def ln_fold_constants(self, gamma: torch.Tensor, beta: torch.Tensor):
+        """``(gamma . W, beta . W)`` f32 [N] for a LayerNorm folded into this layer's input, computed by
+        this layer's own GEMM (so they carry exactly the weights the kernel multiplies: s (q - zp),
+        or fp16((q - zp) s) per group) on [gamma_hi; gamma_lo; beta_hi; beta_lo] f16 rows (hi + lo
+        split: the f32 LayerNorm parameters to ~2^-22)."""
+        rows = []
+        for v in (gamma, beta):
+            v = v.float().reshape(1, -1)
+            hi = v.half()
+            rows += [hi, (v - hi.float()).half()]
+        a = torch.cat(rows).contiguous()
+        out = ops.w4a16_gemm(a, self.prepare(), self.scales, self.qzeros, None, self.outfeatures, self.groupsize,
+                             ops.EPI_F32)
+        return (out[0] + out[1]).contiguous(), (out[2] + out[3]).contiguous()
+
     def forward_epilogue(self, x: torch.Tensor, epilogue: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         assert x.shape[-1] == self.qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
         return ops.w4a16_gemm(x, self.prepare(), self.scales, self.qzeros, self.bias, self.outfeatures,

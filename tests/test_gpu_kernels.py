@@ -383,3 +383,79 @@ def test_conv_ops_reject_bad_shapes(cuda):
     with pytest.raises((AssertionError, NotImplementedError)):
         ops.conv3x3_nhwc(torch.zeros(1, 8, 8, 48, dtype=torch.float16, device=cuda),
                          torch.zeros(128, 3, 3, 48, dtype=torch.float16, device=cuda))
+
+
+# ----------------------------------------------------------------------------- LayerNorm fold
+@pytest.mark.parametrize("groupsize", [-1, 128])
+@pytest.mark.parametrize("m,cfg_p,cfg_c", [(8192, 0, 0), (333, 64, 57), (300, 57, 64)])
+def test_w4a16_gemm_lnf_chain(cuda, groupsize, m, cfg_p, cfg_c):
+    """LayerNorm folded into the GEMMs around it (samq_w4a16_gemm_lnf): the residual producer
+    (x += att.Wp + bp; a = f16((x - mu_p) gamma); per-row partial sums) followed by the consumer
+    (GELU(LN(x).W1 + b1) from a, the sums and gamma.W1 / beta.W1) against the plain fp32 chain
+    x' = x + att.Wp + bp -> LayerNorm -> W1 -> GELU (oracle G1 weights).  mu_p is the previous
+    LayerNorm's mean, here a perturbed copy of the true row mean (what the engine carries)."""
+    import samq
+    from samq import ops
+    c, n1 = 1280, 2560
+    rng = np.random.Generator(np.random.PCG64(5 + m + groupsize))
+    qwp, qzp, scp, bp = _packed_layer(c, c, groupsize, seed=3 + m)
+    qw1, qz1, sc1, b1 = _packed_layer(c, n1, groupsize, seed=4 + m)
+    att = (rng.standard_normal((m, c), dtype=np.float32)).astype(np.float16)
+    x0 = (rng.standard_normal((m, c), dtype=np.float32) * 2 + rng.standard_normal((m, 1), dtype=np.float32) * 3)
+    gamma = (1 + 0.2 * rng.standard_normal(c)).astype(np.float32)
+    beta = (0.1 * rng.standard_normal(c)).astype(np.float32)
+    eps = 1e-6
+    # reference chain (fp32, G1 weights)
+    xr = x0 + gptq_pack.matmul4_g1(att, qwp, scp, qzp, groupsize, bp)
+    mean = xr.mean(1, keepdims=True)
+    ln = (xr - mean) / np.sqrt(xr.var(1, keepdims=True) + eps) * gamma + beta
+    y1 = gptq_pack.matmul4_g1(ln.astype(np.float32), qw1, sc1, qz1, groupsize, b1)
+    ref = sam_ref.gelu_erf(torch.from_numpy(y1)).numpy()
+    # product chain
+    lin_p = samq.QuantLinear(4, groupsize, c, c, True).to(cuda)
+    lin_1 = samq.QuantLinear(4, groupsize, c, n1, True).to(cuda)
+    for lin, (qw, qz, sc, b) in ((lin_p, (qwp, qzp, scp, bp)), (lin_1, (qw1, qz1, sc1, b1))):
+        lin.qweight.copy_(_dev(qw, cuda)); lin.qzeros.copy_(_dev(qz, cuda))
+        lin.scales.copy_(_dev(sc, cuda)); lin.bias.copy_(_dev(b, cuda))
+    lin_p.gemm_cfg, lin_1.gemm_cfg = cfg_p, cfg_c
+    x = _dev(x0, cuda)
+    mu = _dev((mean[:, 0] + 0.05 * rng.standard_normal(m)).astype(np.float32), cuda)
+    stats = torch.empty((m, c // 64, 2), device=cuda)
+    aout = torch.empty((m, c), dtype=torch.float16, device=cuda)
+    g, bt = _dev(gamma, cuda), _dev(beta, cuda)
+    lin_p.forward_lnf(_dev(att, cuda), ops.EPI_RESADD_LNF, x, stats, mu, gamma=g, aout=aout)
+    torch.cuda.synchronize()
+    _close(x, xr, 2e-5 if groupsize == -1 else 4e-3)              # the residual (grouped: fp16 weights)
+    d = x.cpu().numpy() - mu.cpu().numpy()[:, None]                 # the fold algebra on the actual x
+    _close(aout, d * gamma, 2e-3)                                  # f16 fold operand
+    st = stats.cpu().numpy()
+    np.testing.assert_allclose(st[..., 0].sum(1), d.sum(1), rtol=1e-4, atol=1e-2)
+    np.testing.assert_allclose(st[..., 1].sum(1), (d * d).sum(1), rtol=1e-4)
+    gw, bw = lin_1.ln_fold_constants(g, bt)
+    out = torch.empty((m, n1), dtype=torch.float16, device=cuda)
+    mu0 = mu.clone()
+    lin_1.forward_lnf(aout, ops.EPI_GELU_LNF, out, stats, mu, gw=gw, bw=bw, eps=eps)
+    torch.cuda.synchronize()
+    err = _close(out, ref, 4e-3 if groupsize == -1 else 6e-3)
+    print(f"\n[lnf] m={m} g={groupsize}: GELU(LN(x).W1+b1) folded vs fp32 chain max-abs {err:.2e}")
+    np.testing.assert_allclose(mu.cpu().numpy(), mean[:, 0], rtol=0, atol=1e-4)   # mu_p + delta = mean
+    # BIAS_LNF: the same without GELU
+    mu.copy_(mu0)
+    out2 = torch.empty((m, n1), dtype=torch.float16, device=cuda)
+    lin_1.forward_lnf(aout, ops.EPI_BIAS_LNF, out2, stats, mu, gw=gw, bw=bw, eps=eps)
+    torch.cuda.synchronize()
+    _close(out2, y1, 4e-3 if groupsize == -1 else 6e-3)
+
+
+def test_w4a16_gemm_lnf_rejects_non_pingpong(cuda):
+    """The fold epilogues exist only in the ping-pong configs: others are SAMQ_ERR_UNSUPPORTED."""
+    import samq
+    from samq import ops
+    lin = samq.QuantLinear(4, -1, 256, 256, True).to(cuda)
+    lin.gemm_cfg = 22
+    st = torch.zeros((64, 4, 2), device=cuda)
+    mu = torch.zeros(64, device=cuda)
+    with pytest.raises(NotImplementedError):
+        lin.forward_lnf(torch.zeros((64, 256), dtype=torch.float16, device=cuda), ops.EPI_RESADD_LNF,
+                        torch.zeros((64, 256), device=cuda), st, mu, gamma=torch.ones(256, device=cuda),
+                        aout=torch.zeros((64, 256), dtype=torch.float16, device=cuda))
