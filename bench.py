@@ -426,6 +426,8 @@ def main():
                     help="image groups run as concurrent kernel chains on separate HIP streams "
                          "(0 = 2 when the per-GPU batch is even, else 1; W8A8 runs one chain)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fold-ln", action="store_true",
+                    help="W4A16: fold the LayerNorms into the GEMM epilogues (opt-in A/B; measured slower)")
     ap.add_argument("--no-isolated", action="store_true",
                     help="skip the live roofline passes (for a rocprof trace of the timed replays only)")
     ap.add_argument("--backend", default="", help="torch.distributed backend (default nccl = RCCL; gloo for --dry-run)")
@@ -481,6 +483,8 @@ def main():
             cal = torch.randn((1, 3, 1024, 1024), generator=gcal).to(dev, torch.float16)
             samq.calibrate_act_quant(enc, enc.module_forward, [cal])
     eng = enc.engine()
+    if args.fold_ln:
+        eng.fold_ln = True
     log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB "
         f"in {t_bc * 1e3:.1f} ms)")
 

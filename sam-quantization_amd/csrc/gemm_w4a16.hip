@@ -357,54 +357,102 @@ constexpr bool epi_f32_out(int epi) {
   return epi == SAMQ_EPI_RESADD_F32 || epi == SAMQ_EPI_F32 || epi == SAMQ_EPI_RESADD_LNF;
 }
 
-// producer: one f32 residual row chunk (4 columns at col of row) x_new = x + v, its f16 fold
-// operand and this lane's partial sums; the caller reduces the sums over the 16 lanes of a row
+// producer: one f32 residual row chunk (4 columns at col of row) x_new = xo + v (xo: the old
+// residual, loaded ahead by the caller), its f16 fold operand and this lane's partial sums; the
+// caller reduces the sums over the 16 lanes of a row
 __device__ __forceinline__ void lnf_res4(const LnfArgs& L, float* C, int64_t ldc, int N, int64_t row, int col,
-                                         float4_t v, float& s1, float& s2) {
-  float4_t* cp = (float4_t*)(C + row * ldc + col);
-  const float4_t x = *cp + v;
-  *cp = x;
-  const float m = L.mu[row];
-  const float4_t g = *(const float4_t*)(L.gamma + col);
+                                         float4_t xo, float4_t v, float m, float4_t g, float& s1, float& s2) {
+  const float4_t x = xo + v;
+  *(float4_t*)(C + row * ldc + col) = x;
   const float4_t d = x - m;
   *(half4_t*)(L.aout + row * N + col) = half4_t{(_Float16)(d[0] * g[0]), (_Float16)(d[1] * g[1]),
                                                 (_Float16)(d[2] * g[2]), (_Float16)(d[3] * g[3])};
   s1 = (d[0] + d[1]) + (d[2] + d[3]);
   s2 = (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
 }
-// ... reduced over 16 lanes (xor 1, 2, 4, 8: one row), lane 0 of the 16 writes the block's pair
+// sum over the 16 lanes of a DPP row (the xor-1, 2, 4, 8 butterfly's order: same bits)
+__device__ __forceinline__ float sum16_dpp(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x141, 0xF, 0xF, true));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xF, 0xF, true));
+  return v;
+}
+// ... reduced over 16 lanes (one row), lane 0 of the 16 writes the block's pair
 __device__ __forceinline__ void lnf_stats16(const LnfArgs& L, int N, int64_t row, int col_block, bool valid,
                                             float s1, float s2, int c4) {
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    s1 += __shfl_xor(s1, o, 64);
-    s2 += __shfl_xor(s2, o, 64);
-  }
+  s1 = sum16_dpp(s1);
+  s2 = sum16_dpp(s2);
   if (valid && c4 == 0) *(float2_t*)(L.stats + (row * (N / 64) + col_block) * 2) = float2_t{s1, s2};
 }
-// consumer: (delta, rstd) of the wave's WM rows into LDS (rowinfo), mu += delta by column block 0
-template <int WM>
-__device__ __forceinline__ void lnf_rowinfo(const LnfArgs& L, float2_t* rowinfo, int M, int row_base, bool col0,
-                                            int lane) {
-  const float inv_k = 1.0f / (float)(L.nblk * 64);
+// producer slice of R rows x 64 columns staged in LDS at ep (row pitch P floats): the old residual
+// and the row means are all loaded before the first store (no store-to-load ordering per chunk)
+template <int R, int P>
+__device__ __forceinline__ void lnf_produce_slice(const LnfArgs& L, const float* ep, float* C, int64_t ldc, int N,
+                                                  int M, int srow0, int col_base, int lane) {
+  constexpr int J = R * 16 / 64;
+  const int c4 = lane & 15;
+  const int col = col_base + 4 * c4;
+  const float4_t g = *(const float4_t*)(L.gamma + col);
+  float4_t xo[J];
+  float m[J];
 #pragma unroll
-  for (int q = 0; q < WM / 64; ++q) {
-    const int rl = q * 64 + lane;
-    const int64_t row = row_base + rl;
+  for (int j = 0; j < J; ++j) {
+    int64_t row = srow0 + 4 * j + (lane >> 4);
+    row = row < M ? row : M - 1;
+    xo[j] = *(const float4_t*)(C + row * ldc + col);
+    m[j] = L.mu[row];
+  }
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int rl = 4 * j + (lane >> 4);
+    const int row = srow0 + rl;
+    const float4_t v = *(const float4_t*)(ep + rl * P + 4 * c4);
     float s1 = 0.f, s2 = 0.f;
-    if (row < M) {
-      const float2_t* sp = (const float2_t*)(L.stats + row * L.nblk * 2);
+    if (row < M) lnf_res4(L, C, ldc, N, row, col, xo[j], v, m[j], g, s1, s2);
+    lnf_stats16(L, N, row, col_base / 64, row < M, s1, s2, c4);
+  }
+}
+// consumer: (delta, rstd) of the workgroup's BM rows into LDS (rowinfo[BM]), mu += delta by the
+// workgroups of column tile 0.  The rows' partial sums (BM x nblk float2, contiguous) arrive by
+// LDS-DMA (1 KiB pieces dealt over the NW waves, one wait), then one lane per row adds its nblk
+// pairs in block order from LDS (the order of the standalone reduction: same bits).
+template <int BM, int NW>
+__device__ __forceinline__ void lnf_rowinfo_wg(const LnfArgs& L, float2_t* rowinfo, char* sbuf, int M, int row_base,
+                                               bool col0, int wave, int lane) {
+  static_assert(BM % (NW * 32) == 0 || BM <= NW * 64, "rows per wave");
+  const int nfl = 2 * L.nblk;                                 // floats per row
+  const int npieces = BM * nfl / 256;                         // 1 KiB pieces (BM * nblk * 8 / 1024)
+  const float* base = L.stats + (int64_t)row_base * nfl;
+  const int64_t lim = (int64_t)(M - row_base) * nfl - 4;      // last in-bounds 16-byte chunk
+  for (int pc = wave; pc < npieces; pc += NW) {
+    int64_t off = (int64_t)(pc * 64 + lane) * 4;
+    off = off <= lim ? off : lim;
+    __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(base + off), (SAMQ_LDS void*)(sbuf + pc * 1024), 16, 0, 0);
+  }
+  vm_wait<0>();
+  __syncthreads();
+  const float inv_k = 1.0f / (float)(L.nblk * 64);
+  constexpr int RPW = BM / NW;                                // rows per wave
+#pragma unroll
+  for (int q = 0; q < (RPW + 63) / 64; ++q) {
+    const int rl = wave * RPW + q * 64 + lane;
+    if (q * 64 + lane < RPW) {
+      const float2_t* sp = (const float2_t*)(sbuf + rl * nfl * 4);
+      float s1 = 0.f, s2 = 0.f;
       for (int b = 0; b < L.nblk; ++b) {
         const float2_t v = sp[b];
         s1 += v.x;
         s2 += v.y;
       }
+      const float delta = s1 * inv_k;
+      const float var = fmaxf(s2 * inv_k - delta * delta, 0.0f);
+      rowinfo[rl] = float2_t{delta, rsqrtf(var + L.eps)};
+      const int64_t row = row_base + rl;
+      if (col0 && row < M) L.mu[row] += delta;
     }
-    const float delta = s1 * inv_k;
-    const float var = fmaxf(s2 * inv_k - delta * delta, 0.0f);
-    rowinfo[rl] = float2_t{delta, rsqrtf(var + L.eps)};
-    if (col0 && row < M) L.mu[row] += delta;
   }
+  __syncthreads();
 }
 // consumer store of 8 columns: y = rstd * (v - delta * gw) + (bw + bias) (-> GELU), f16
 template <int EPI>
@@ -459,18 +507,7 @@ __device__ __forceinline__ void pp_epilogue16(const float4_t (&acc)[TM16][TN][2]
     __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
     const int srow0 = row_base + i * 16;
     if (lnf_producer(EPI)) {
-      constexpr int C4 = WN / 4;
-      static_assert((EP_ROWS * C4) % 64 == 0, "LN fold: whole waves per slice");
-#pragma unroll
-      for (int j = 0; j < EP_ROWS * C4 / 64; ++j) {
-        const int idx = j * 64 + lane;
-        const int rl = idx / C4, c4 = idx % C4;
-        const int row = srow0 + rl;
-        const float4_t v = *(const float4_t*)(ep + rl * PITCH + 4 * c4);
-        float s1 = 0.f, s2 = 0.f;
-        if (row < M) lnf_res4(L, (float*)Cout, ldc, N, row, col_base + 4 * c4, v, s1, s2);
-        lnf_stats16(L, N, row, col_base / 64, row < M, s1, s2, c4);
-      }
+      lnf_produce_slice<EP_ROWS, PITCH>(L, ep, (float*)Cout, ldc, N, M, srow0, col_base, lane);
     } else if (EPI == SAMQ_EPI_RESADD_F32 || EPI == SAMQ_EPI_F32) {
       constexpr int C4 = WN / 4;
 #pragma unroll
@@ -971,18 +1008,7 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
       const int srow0 = row_base + i * 32 + sl * EP_ROWS;
       if (lnf_producer(EPI)) {
-        constexpr int C4 = WN / 4;
-        static_assert((EP_ROWS * C4) % 64 == 0, "LN fold: whole waves per slice");
-#pragma unroll
-        for (int j = 0; j < EP_ROWS * C4 / 64; ++j) {
-          const int idx = j * 64 + lane;
-          const int rl = idx / C4, c4 = idx % C4;
-          const int row = srow0 + rl;
-          const float4_t v = ((const float4_t*)ep)[idx];
-          float s1 = 0.f, s2 = 0.f;
-          if (row < M) lnf_res4(L, (float*)Cout, ldc, N, row, col_base + 4 * c4, v, s1, s2);
-          lnf_stats16(L, N, row, col_base / 64, row < M, s1, s2, c4);
-        }
+        lnf_produce_slice<EP_ROWS, WN>(L, ep, (float*)Cout, ldc, N, M, srow0, col_base, lane);
       } else if (lnf_consumer(EPI)) {
         constexpr int C8 = WN / 8;
 #pragma unroll
@@ -1156,7 +1182,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   constexpr int EP_ROWS = WN > 64 ? 16 : 32;
   constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : EP_ROWS * WN * 4;
   // LN-fold consumers: per-wave (delta, rstd) of its WM rows behind the epilogue slices
-  constexpr int RI_BYTES = lnf_consumer(EPI) ? NW * WM * 8 : 0;
+  constexpr int RI_BYTES = lnf_consumer(EPI) ? BM * 8 : 0;
   constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES + RI_BYTES ? STAGES * STAGE : NW * EP_BYTES + RI_BYTES;
   static_assert(!M16 || NPH <= 2, "M16: one or two phases per K tile");
   static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
@@ -1520,12 +1546,11 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
         cb16[t][h] = bias ? (float)bias[c] : 0.0f;
       }
     __syncthreads();
-    float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES + wave * WM * 8);
+    float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES) + wm * WM;
     lnf.bias = bias;
-    if constexpr (lnf_consumer(EPI)) {
-      lnf_rowinfo<WM>(lnf, rowinfo, M, m0 + wm * WM, n0 + wn * WN == 0, lane);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-    }
+    if constexpr (lnf_consumer(EPI))
+      lnf_rowinfo_wg<BM, NW>(lnf, (float2_t*)(smem + NW * EP_BYTES), smem + NW * EP_BYTES + RI_BYTES, M, m0, n0 == 0,
+                             wave, lane);
     pp_epilogue16<2 * TM, TN, EPI>(acc16, csc16, cb16, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
                                    n0 + wn * WN, lane, lnf, N, rowinfo);
     return;
@@ -1537,12 +1562,11 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     cb[t] = bias ? (float)bias[col[t]] : 0.0f;
   }
   __syncthreads();
-  float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES + wave * WM * 8);
+  float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES) + wm * WM;
   lnf.bias = bias;
-  if constexpr (lnf_consumer(EPI)) {
-    lnf_rowinfo<WM>(lnf, rowinfo, M, m0 + wm * WM, n0 + wn * WN == 0, lane);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-  }
+  if constexpr (lnf_consumer(EPI))
+    lnf_rowinfo_wg<BM, NW>(lnf, (float2_t*)(smem + NW * EP_BYTES), smem + NW * EP_BYTES + RI_BYTES, M, m0, n0 == 0,
+                           wave, lane);
   pp_epilogue<TM, TN, EP_ROWS, EPI>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
                                     n0 + wn * WN, lane, lnf, N, rowinfo);
 }
@@ -1858,6 +1882,9 @@ extern "C" int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wp
     SAMQ_REQUIRE(gamma && aout, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: the producer needs gamma and aout");
   } else if (epilogue == SAMQ_EPI_BIAS_LNF || epilogue == SAMQ_EPI_GELU_LNF) {
     SAMQ_REQUIRE(gw && bw, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: the consumer needs gw and bw");
+    // the workgroup's row partial sums (256 rows x K/64 pairs) are staged in the LDS the ring
+    // leaves free in the epilogue (>= 94 KiB on both ping-pong forms)
+    SAMQ_REQUIRE(K <= 2048, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: consumer K must be <= 2048");
   } else {
     return fail(SAMQ_ERR_INVALID, "w4a16_gemm_lnf: epilogue must be RESADD_LNF, BIAS_LNF or GELU_LNF");
   }

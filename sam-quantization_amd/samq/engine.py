@@ -48,8 +48,10 @@ class EncoderEngine:
         self.grid = enc.img_size // enc.patch_size
         self.ln_rpw = 0   # LayerNorm rows per wave (0 = library default; in-graph A/B knob)
         # fold norm2 / the next block's norm1 into the GEMMs around them (W4A16, >= 8192 rows per
-        # chain: the ping-pong GEMMs carry the fold epilogues); False = standalone LayerNorms
-        self.fold_ln = True
+        # chain: the ping-pong GEMMs carry the fold epilogues).  Off by default: measured in the
+        # 2-lane bench graph the fold epilogues cost more than the two LayerNorm launches they
+        # replace (isolated per block 358 vs 351 us, step 23.4 vs 23.0 ms)
+        self.fold_ln = False
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
