@@ -502,7 +502,8 @@ def main():
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
-    if world > 1:
+    on = dist.is_available() and dist.is_initialized()   # also a forced one-rank RCCL group
+    if on:
         dist.barrier()
     torch.cuda.synchronize()
     rtx = _roctx()   # marks the timed window for tools/instep_profile.sh (no-op unprofiled)
@@ -514,10 +515,10 @@ def main():
     torch.cuda.synchronize()
     if rtx:
         rtx.roctxRangePop()
-    if world > 1:
+    if on:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
+    if on:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
@@ -585,7 +586,7 @@ def main():
             "e2e": {"tflop_per_image": round(fl["total"] / 1e12, 4), "achieved_tflops_per_gpu": round(e2e_tflops, 1),
                     "frac_of_fp16_peak": round(e2e_tflops / PEAK_FP16_TFLOPS, 4),
                     "frac_of_int8_peak": round(e2e_tflops / (2 * PEAK_FP16_TFLOPS), 4)},
-            "dist": {"backend": dist.get_backend() if world > 1 else None, "world_size_seen": world,
+            "dist": {"backend": dist.get_backend() if on else None, "world_size_seen": world,
                      "broadcast_bytes": nbytes, "broadcast_ms": round(t_bc * 1e3, 2),
                      "rank0_shard": [start, stop]},
         }

@@ -107,6 +107,7 @@ int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, cons
 #define SAMQ_EPI_RESADD_LNF 7
 #define SAMQ_EPI_BIAS_LNF 8
 #define SAMQ_EPI_GELU_LNF 9
+#define SAMQ_EPI_SILU_MUL 10   /* internal: the samq_w4a16_gated_mlp epilogue */
 /* samq_w4a16_gemm_cfg with the LayerNorm-fold epilogues above (ping-pong configs 57 / 64 / 0 =
  * automatic at M >= 8192 only, else SAMQ_ERR_UNSUPPORTED): gamma f32 [N] (producer), gw / bw f32
  * [N] (consumer), stats f32, mu f32 [M], aout f16 [M,N] (producer), eps of the folded LayerNorm. */
@@ -186,6 +187,17 @@ int samq_quantize(const void* x, void* y, int64_t n, float scale, int flags, hip
 size_t samq_minmax_workspace(int64_t rows, int C, int axis);
 int samq_minmax(const void* x, int64_t rows, int C, int in_f16, int axis, float* max_io, float* min_io,
                 int init, float* workspace, size_t workspace_floats, hipStream_t stream);
+
+/* Fused gated MLP in ONE launch: C f16 [M, N] = silu(A . Wg) * (A . Wu) with both int4 weight
+ * sets in one packed matrix of 2N columns whose 32-column blocks alternate gate block j, up
+ * block j (the samq_w4_repack layout-1 blocks interleaved; scales / qzeros interleaved the same
+ * way, N2 = 2N, N2 % 256 == 0): each wave's 64-column tile holds a gate block and its up block,
+ * the epilogue multiplies them in registers.  fp32 accumulate, exact integer weights (G1).
+ * Replaces llama_mlp_fused_4_kernel / triton_llama_mlp_4 (gptq_triton/fused_mlp.py:230-388,
+ * 391-477); biases are ignored as there. */
+int samq_w4a16_gated_mlp(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                         const int32_t* qzeros, void* C, int64_t ldc, int M, int N2, int K, int groupsize,
+                         hipStream_t stream);
 
 /* Gated-MLP activation: out f16[i] = silu(gate[i]) * up[i] (f32 inputs).  With two
  * samq_w4a16_gemm(..., SAMQ_EPI_F32) calls it replaces triton_llama_mlp_4 /

@@ -979,6 +979,38 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
   static_assert(!(lnf_producer(EPI) || lnf_consumer(EPI)) || WN == 64, "LN fold: 64-column wave tiles");
   float* ep = (float*)ep_bytes;
   const int hsel = lane >> 5;
+  if constexpr (EPI == SAMQ_EPI_SILU_MUL) {
+    // gated MLP: the wave's 64 columns are one 32-column block of the gate (t = 0) and the same
+    // block of the up projection (t = 1) -- samq_w4_interleave32 layout; out f16 [M, N / 2] =
+    // silu(gate) * up, the 32 output columns of block (col_base / 64)
+    static_assert(TN == 2 && EP_ROWS == 32, "SILU_MUL: 64-column wave tiles");
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        const float gv = acc[i][0][r] * csc[0], uv = acc[i][1][r] * csc[1];
+        ep[rl * 32 + (lane & 31)] = gv / (1.0f + __expf(-gv)) * uv;
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      const int srow0 = row_base + i * 32;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {   // 32 rows x 4 chunks of 8 columns
+        const int idx = j * 64 + lane;
+        const int rl = idx >> 2, c8 = idx & 3;
+        const int row = srow0 + rl;
+        const float4_t v0 = ((const float4_t*)ep)[2 * idx];
+        const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+        if (row < M) {
+          const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
+                             (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
+          *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base / 2 + 8 * c8) = h;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+    return;
+  }
   float gw8[8], bb8[8];   // LNF consumer: this lane's 8 columns (fixed over the slices)
   if constexpr (lnf_consumer(EPI)) {
     const int c0 = col_base + 8 * (lane % (WN / 8));
@@ -1628,6 +1660,13 @@ static int launch_lnf(const GemmArgs& a, int cfg, hipStream_t st) {
   return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm_lnf: the LayerNorm fold needs ping-pong config 57 or 64");
 }
 
+// gated-MLP epilogue: the 32x32x16 ping-pong config (57) only
+template <bool GR>
+static int launch_silu(const GemmArgs& a, hipStream_t st) {
+  if (GR) return launch_pp2<2, 4, 2, 2, 3, 2, SAMQ_EPI_SILU_MUL, 512>(a, st);
+  return launch_pp2<2, 4, 2, 2, 4, 3, SAMQ_EPI_SILU_MUL, 4096>(a, st);
+}
+
 template <int EPI, bool GR>
 static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
   if (cfg >= 50 && cfg < 100) {   // ping-pong kernels
@@ -1860,6 +1899,24 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
     case SAMQ_EPI_F32: return gr ? launch_epi<SAMQ_EPI_F32, true>(a, cfg, stream) : launch_epi<SAMQ_EPI_F32, false>(a, cfg, stream);
     default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: unknown epilogue");
   }
+}
+
+extern "C" int samq_w4a16_gated_mlp(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
+                                    const int32_t* qzeros, void* C, int64_t ldc, int M, int N2, int K, int groupsize,
+                                    hipStream_t stream) {
+  SAMQ_REQUIRE(A && wpacked && scales && qzeros && C, SAMQ_ERR_INVALID, "w4a16_gated_mlp: null pointer");
+  SAMQ_REQUIRE(M >= 0 && N2 > 0 && K > 0 && K % 64 == 0, SAMQ_ERR_INVALID,
+               "w4a16_gated_mlp: K must be a positive multiple of 64");
+  SAMQ_REQUIRE(N2 % 256 == 0, SAMQ_ERR_INVALID, "w4a16_gated_mlp: 2N must be a multiple of 256");
+  SAMQ_REQUIRE(lda >= K && lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ldc >= N2 / 2 && ldc % 8 == 0 &&
+               ((uintptr_t)C & 15) == 0, SAMQ_ERR_INVALID, "w4a16_gated_mlp: 16-byte aligned A / C rows required");
+  if (groupsize == -1) groupsize = K;
+  SAMQ_REQUIRE(groupsize > 0 && (groupsize == K || groupsize % 64 == 0), SAMQ_ERR_INVALID,
+               "w4a16_gated_mlp: groupsize must be -1, K, or a multiple of 64");
+  if (M == 0) return SAMQ_OK;
+  GemmArgs a{(const _Float16*)A, lda, (const u32x4*)wpacked, (const _Float16*)scales, (const uint32_t*)qzeros,
+             nullptr, C, ldc, M, N2, K, groupsize};
+  return groupsize != K ? launch_silu<true>(a, stream) : launch_silu<false>(a, stream);
 }
 
 extern "C" int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,

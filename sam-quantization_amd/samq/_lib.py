@@ -75,6 +75,7 @@ SIGNATURES = {
     "samq_minmax_workspace": (ctypes.c_size_t, [_i64, _i32, _i32]),
     "samq_minmax": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, ctypes.c_size_t, _vp]),
     "samq_silu_mul": (_i32, [_vp, _vp, _vp, _i64, _vp]),
+    "samq_w4a16_gated_mlp": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _vp]),
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
     "samq_layernorm_mean": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp]),
     "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),

@@ -12,10 +12,14 @@ import torch
 import torch.distributed as dist
 
 
-def init_from_env(backend: str | None = None):
-    """``torch.distributed`` from torchrun's RANK / WORLD_SIZE / LOCAL_RANK (no-op if unset)."""
+def init_from_env(backend: str | None = None, force: bool | None = None):
+    """``torch.distributed`` from torchrun's RANK / WORLD_SIZE / LOCAL_RANK (no-op if unset, and for
+    a world of one unless ``force`` / ``SAMQ_DIST_FORCE=1``: a one-rank RCCL group runs the same
+    communicator set-up and collectives as N ranks -- the single-GPU hardware check of this path)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1 or dist.is_initialized():
+    if force is None:
+        force = os.environ.get("SAMQ_DIST_FORCE", "") == "1" and "RANK" in os.environ
+    if (ws <= 1 and not force) or dist.is_initialized():
         return (dist.get_rank(), dist.get_world_size()) if dist.is_initialized() else (0, 1)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
@@ -37,7 +41,7 @@ def _buckets(tensors):
 def broadcast_state(module: torch.nn.Module, src: int = 0) -> int:
     """Broadcast every parameter and persistent buffer of ``module`` from ``src`` with one
     collective per dtype (flattened buckets).  Returns the number of bytes broadcast."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return 0
     tensors = [t for t in module.state_dict().values() if torch.is_tensor(t)]
     total = 0
@@ -64,7 +68,7 @@ def shard(n_items: int, rank: int, world: int):
 
 def gather_embeddings(local: torch.Tensor, dst: int = 0):
     """Gather per-rank outputs (equal shapes) onto ``dst``; returns the concatenation there."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return local
     parts = [torch.empty_like(local) for _ in range(dist.get_world_size())] if dist.get_rank() == dst else None
     dist.gather(local, parts, dst=dst)

@@ -4,9 +4,11 @@ The reference fuses ``silu(A . Wgate) * (A . Wup)`` for LLaMA MLPs (``fused_mlp.
 ``make_fused_mlp`` ``:13-27``, ``autotune_warmup`` ``:30-71``, ``QuantLlamaMLP`` ``:74-112``,
 ``llama_mlp_fused_4_kernel`` ``:230-383``, ``triton_llama_mlp_4`` ``:391-477``).  SAM has no such
 MLP (its ``make_fused_mlp`` even references an undefined ``LlamaMLP``); this module keeps the
-names, arguments, buffers and asserts so code written against it runs: two int4 GEMMs with the
-f32 epilogue (exact integer weights, fp32 accumulate, G1 numerics) and one HIP ``silu * up``
-pass.  Biases of gate/up are ignored, as in the reference kernel.
+names, arguments, buffers and asserts so code written against it runs, and fuses like the
+reference: both int4 GEMMs and ``silu(g) * u`` in ONE launch (``samq_w4a16_gated_mlp``: the two
+packed weights interleaved in 32-column blocks, so each wave tile holds a gate block and its up
+block and the epilogue multiplies them in registers; exact integer weights, fp32 accumulate, G1
+numerics).  Biases of gate/up are ignored, as in the reference kernel.
 """
 from __future__ import annotations
 
@@ -18,10 +20,18 @@ import torch.nn as nn
 from . import _lib, ops
 
 
+def _gated_operands(gate_qweight, gate_scales, gate_qzeros, up_qweight, up_scales, up_qzeros):
+    n = gate_qweight.shape[1]
+    return ops.w4_interleave32(ops.w4_repack(gate_qweight), ops.w4_repack(up_qweight), gate_scales, up_scales,
+                               gate_qzeros, up_qzeros, n)
+
+
 def triton_llama_mlp_4(groupsize: int, a: torch.Tensor, gate_qweight: torch.Tensor, gate_scales: torch.Tensor,
                        gate_qzeros: torch.Tensor, up_qweight: torch.Tensor, up_scales: torch.Tensor,
-                       up_qzeros: torch.Tensor) -> torch.Tensor:
-    """``silu(gate(a)) * up(a)``, a (..., K) fp16 -> (..., N) fp16 (reference ``:391-477``)."""
+                       up_qzeros: torch.Tensor, _operands=None) -> torch.Tensor:
+    """``silu(gate(a)) * up(a)``, a (..., K) fp16 -> (..., N) fp16 (reference ``:391-477``): both
+    int4 GEMMs and the gate product in one HIP launch (samq_w4a16_gated_mlp; ``_operands`` = the
+    cached ``ops.w4_interleave32`` buffers of a ``QuantLlamaMLP``)."""
     assert (gate_qweight.shape == up_qweight.shape and gate_scales.shape == up_scales.shape
             and gate_qzeros.shape == up_qzeros.shape), "All weights must have the same shape"
     assert a.shape[-1] == gate_qweight.shape[0] * 8, "A must be a multiple of 8 in the last dimension"
@@ -32,13 +42,9 @@ def triton_llama_mlp_4(groupsize: int, a: torch.Tensor, gate_qweight: torch.Tens
     gs = k if groupsize == -1 else groupsize
     assert gs % 128 == 0, "groupsize must be a multiple of 32, 64, and 128"
     gs = -1 if gs == k else gs
-    x = a.view(-1, k)
-    g = ops.w4a16_gemm(x, ops.w4_repack(gate_qweight), gate_scales, gate_qzeros, None, n, gs, ops.EPI_F32)
-    u = ops.w4a16_gemm(x, ops.w4_repack(up_qweight), up_scales, up_qzeros, None, n, gs, ops.EPI_F32)
-    c = torch.empty((x.shape[0], n), dtype=torch.float16, device=a.device)
-    _lib.check(_lib.load().samq_silu_mul(g.data_ptr(), u.data_ptr(), c.data_ptr(), c.numel(), ops._stream()),
-               "silu_mul")
-    return c.view(a.shape[:-1] + (n,))
+    w2, s2, z2 = _operands if _operands is not None else _gated_operands(
+        gate_qweight, gate_scales, gate_qzeros, up_qweight, up_scales, up_qzeros)
+    return ops.w4a16_gated_mlp(a, w2, s2, z2, n, gs)
 
 
 llama_mlp_4 = triton_llama_mlp_4
@@ -62,11 +68,19 @@ class QuantLlamaMLP(nn.Module):
         self.outfeatures = down_proj.outfeatures
         self.down_proj = down_proj
 
+    def gated_operands(self):
+        """The interleaved gate/up operands of the fused kernel, built once per device."""
+        key = self.gate_proj_qweight.device
+        if getattr(self, "_gated", None) is None or self._gated[0] != key:
+            self._gated = (key, _gated_operands(self.gate_proj_qweight, self.gate_proj_scales, self.gate_proj_qzeros,
+                                                self.up_proj_qweight, self.up_proj_scales, self.up_proj_qzeros))
+        return self._gated[1]
+
     def forward(self, x):
         gs = -1 if self.groupsize == self.infeatures else self.groupsize
         return self.down_proj(triton_llama_mlp_4(gs, x, self.gate_proj_qweight, self.gate_proj_scales,
                                                  self.gate_proj_qzeros, self.up_proj_qweight, self.up_proj_scales,
-                                                 self.up_proj_qzeros))
+                                                 self.up_proj_qzeros, _operands=self.gated_operands()))
 
 
 def make_fused_mlp(m: nn.Module, parent_name: str = "") -> nn.Module:

@@ -84,6 +84,39 @@ def w4a16_gemm(a: torch.Tensor, wpacked: torch.Tensor, scales: torch.Tensor, qze
     return out
 
 
+def w4_interleave32(gate_packed: torch.Tensor, up_packed: torch.Tensor, gate_scales: torch.Tensor,
+                    up_scales: torch.Tensor, gate_qzeros: torch.Tensor, up_qzeros: torch.Tensor, n: int):
+    """The samq_w4a16_gated_mlp operand layout: two repacked (layout 1) int4 matrices of N columns
+    -> one of 2N whose 32-column blocks alternate gate block j / up block j (each block is one
+    contiguous run of K/64 KiB in the repacked layout), scales (G, N) / qzeros (G, N/8) the same."""
+    _need_cuda(gate_packed, up_packed, gate_scales, up_scales, gate_qzeros, up_qzeros)
+    assert n % 32 == 0 and gate_packed.numel() == up_packed.numel()
+    nb = n // 32
+    w = torch.stack([gate_packed.view(nb, -1), up_packed.view(nb, -1)], 1).reshape(-1).contiguous()
+    g = gate_scales.shape[0]
+    s = torch.stack([gate_scales.reshape(g, nb, 32), up_scales.reshape(g, nb, 32)], 2).reshape(g, 2 * n).contiguous()
+    z = torch.stack([gate_qzeros.reshape(g, nb, 4), up_qzeros.reshape(g, nb, 4)], 2).reshape(g, n // 4).contiguous()
+    return w, s, z
+
+
+def w4a16_gated_mlp(a: torch.Tensor, wpacked2: torch.Tensor, scales2: torch.Tensor, qzeros2: torch.Tensor,
+                    n: int, groupsize: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``silu(a . Wgate) * (a . Wup)`` f16 (..., N) in ONE launch (samq_w4a16_gated_mlp) from the
+    ``w4_interleave32`` operands of the two projections."""
+    _need_cuda(a, wpacked2, scales2, qzeros2)
+    assert a.dtype == torch.float16 and a.stride(-1) == 1
+    k = a.shape[-1]
+    x = a.reshape(-1, k)
+    m = x.shape[0]
+    if out is None:
+        out = torch.empty(a.shape[:-1] + (n,), dtype=torch.float16, device=a.device)
+    assert out.is_contiguous() and out.dtype == torch.float16 and out.numel() == m * n
+    _lib.check(_lib.load().samq_w4a16_gated_mlp(_ptr(x), x.stride(0), _ptr(wpacked2), _ptr(scales2), _ptr(qzeros2),
+                                                _ptr(out), n, m, 2 * n, k, groupsize, _stream()),
+               "w4a16_gated_mlp")
+    return out
+
+
 def w4a16_gemm_lnf(a: torch.Tensor, wpacked: torch.Tensor, scales: torch.Tensor, qzeros: torch.Tensor,
                    bias: Optional[torch.Tensor], n: int, groupsize: int, epilogue: int, out: torch.Tensor,
                    stats: torch.Tensor, mu: torch.Tensor, gamma: Optional[torch.Tensor] = None,

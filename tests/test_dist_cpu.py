@@ -96,3 +96,21 @@ def test_bench_launches_its_own_ranks_and_shards_the_global_batch():
     ref = bench.local_images(0, 6, torch.device("cpu"), torch.float32, size=32)
     got = ranks[0]["image_checksums"] + ranks[1]["image_checksums"]
     assert got == [float(x.double().sum()) for x in ref]
+
+
+def test_forced_one_rank_group_runs_the_collectives():
+    """``SAMQ_DIST_FORCE=1`` under a one-rank torchrun environment initialises the process group
+    (gloo here; RCCL in tests/test_dist_gpu.py) and the weight broadcast / gather go through it."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), SAMQ_DIST_FORCE="1")
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "1", "--backend", "gloo", "--dry-run",
+                        "--batch", "2"], capture_output=True, text=True, timeout=300, env=env, cwd=str(repo))
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["backend"] == "gloo" and out["world_size_seen"] == 1
+    assert out["ranks"][0]["broadcast_bytes"] > 0 and out["ranks"][0]["shard"] == [0, 2]

@@ -41,10 +41,11 @@ def test_fused_mlp_asserts_and_swap_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("groupsize", [-1, 128])
-def test_triton_llama_mlp_4_vs_oracle(cuda, groupsize):
+@pytest.mark.parametrize("groupsize,m", [(-1, 77), (128, 77), (-1, 1), (128, 300), (-1, 1000)])
+def test_triton_llama_mlp_4_vs_oracle(cuda, groupsize, m):
+    """One fused launch (samq_w4a16_gated_mlp) vs the fp32 oracle, M from decode (1) to 1000."""
     from samq.fused_mlp import triton_llama_mlp_4
-    k, n, m = 1024, 768, 77
+    k, n = 1024, 768
     g, u = _packed(k, n, 3, groupsize), _packed(k, n, 4, groupsize)
     rng = np.random.Generator(np.random.PCG64(5))
     a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
@@ -57,3 +58,45 @@ def test_triton_llama_mlp_4_vs_oracle(cuda, groupsize):
     assert out.shape == (1, m, n) and out.dtype == torch.float16
     err = np.abs(out.float().cpu().numpy()[0] - ref).max()
     assert err <= 2e-3 * max(1.0, np.abs(ref).max()), err
+
+
+@pytest.mark.gpu
+def test_gated_mlp_one_launch_matches_two_gemms_and_module(cuda):
+    """The fused kernel equals the unfused composition (two EPI_F32 int4 GEMMs + samq_silu_mul) up
+    to fp16 output rounding, and QuantLlamaMLP.forward (cached interleaved operands) runs it."""
+    import samq
+    from samq import _lib, ops
+    from samq.fused_mlp import QuantLlamaMLP
+    k, n, m = 512, 1024, 4096
+    g, u = _packed(k, n, 6), _packed(k, n, 7)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(cuda)  # noqa: E731
+    a = (torch.randn(m, k, generator=torch.Generator().manual_seed(3)) * 0.5).half().to(cuda)
+    gp, up = ops.w4_repack(t(g[0])), ops.w4_repack(t(u[0]))
+    w2, s2, z2 = ops.w4_interleave32(gp, up, t(g[2]), t(u[2]), t(g[1]), t(u[1]), n)
+    fused = ops.w4a16_gated_mlp(a, w2, s2, z2, n, -1)
+    xg = ops.w4a16_gemm(a, gp, t(g[2]), t(g[1]), None, n, -1, ops.EPI_F32)
+    xu = ops.w4a16_gemm(a, up, t(u[2]), t(u[1]), None, n, -1, ops.EPI_F32)
+    ref = torch.empty(m, n, dtype=torch.float16, device=cuda)
+    _lib.check(_lib.load().samq_silu_mul(xg.data_ptr(), xu.data_ptr(), ref.data_ptr(), ref.numel(), ops._stream()),
+               "silu_mul")
+    d = (fused.float() - ref.float()).abs()
+    tol = 2e-3 * ref.float().abs() + 1e-3
+    assert bool((d <= tol).all()), float(d.max())
+
+    gate = samq.QuantLinear(4, -1, k, n, False).to(cuda)
+    upl = samq.QuantLinear(4, -1, k, n, False).to(cuda)
+    down = samq.QuantLinear(4, -1, n, k, False).to(cuda)
+    for lin, pk in ((gate, g), (upl, u)):
+        lin.qweight.copy_(t(pk[0]))
+        lin.qzeros.copy_(t(pk[1]))
+        lin.scales.copy_(t(pk[2]))
+    dq, dz, ds = _packed(n, k, 8)
+    down.qweight.copy_(t(dq))
+    down.qzeros.copy_(t(dz))
+    down.scales.copy_(t(ds))
+    mlp = QuantLlamaMLP(gate, down, upl)
+    y = mlp(a.view(2, m // 2, k))
+    y_ref = down(ref.view(2, m // 2, n))
+    assert y.shape == (2, m // 2, k)
+    assert (y.float() - y_ref.float()).abs().max().item() <= 5e-3 * max(1.0, y_ref.float().abs().max().item())
+    assert mlp._gated is not None and mlp(a.view(2, m // 2, k)).equal(y)
