@@ -383,33 +383,36 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   const int64_t ts = 3 * (int64_t)C;
   const int8_t* img = p.qkv + (int64_t)b * G * G * ts;
 
-  // ---- K / V staging: piece u = key * 4 + part (16 bytes of dims 16 part .. +15)
-  u32x4 kreg[UPT], vreg[UPT];
-  auto load = [&](int kh) {
+  // ---- K / V staging: piece u = key * 4 + part (16 bytes of dims 16 part .. +15).  Two register
+  // sets: chunk ch + 2 is loaded while chunk ch is computed and chunk ch + 1 (loaded one chunk
+  // earlier) is stored -- two chunks of math to cover each load's latency
+  u32x4 kreg[2][UPT], vreg[2][UPT];
+  auto load = [&](int kh, int r) {
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const int u = tid + j * NT, key = u >> 2, part = u & 3;
       const int8_t* tp = img + ((int64_t)kh * G + key) * ts + head * QD + part * 16;
-      kreg[j] = *(const u32x4*)(tp + C);
-      vreg[j] = *(const u32x4*)(tp + 2 * C);
+      kreg[r][j] = *(const u32x4*)(tp + C);
+      vreg[r][j] = *(const u32x4*)(tp + 2 * C);
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, int r) {
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const int u = tid + j * NT, key = u >> 2, part = u & 3;
-      *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kreg[j];
+      *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kreg[r][j];
       half8_t h0, h1;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        h0[e] = (_Float16)(float)(int8_t)((vreg[j][e >> 2] >> (8 * (e & 3))) & 0xFFu);
-        h1[e] = (_Float16)(float)(int8_t)((vreg[j][2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
+        h0[e] = (_Float16)(float)(int8_t)((vreg[r][j][e >> 2] >> (8 * (e & 3))) & 0xFFu);
+        h1[e] = (_Float16)(float)(int8_t)((vreg[r][j][2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
       }
       *(half8_t*)(&v_lds[buf][key * VP + part * 16]) = h0;
       *(half8_t*)(&v_lds[buf][key * VP + part * 16 + 8]) = h1;
     }
   };
-  load(0);
+  load(0, 0);
+  load(1, 1);
 
   // ---- this wave's 16 queries (codes) and their rel-pos terms: fp32 dot products of the
   // fake-quant q with the f32 tables (rows qy - k + 63 for both, quirk 1).  Lane (g, ql) computes
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
       rwr[bb][i] = rw4[i];
     }
   }
-  store(0);
+  store(0, 0);
   __syncthreads();   // chunk 0 staged; the rel_h rows visible
   const float* rhq = &rh_lds[wave][ql * (G + 1)];
 
@@ -451,9 +454,11 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
 #pragma unroll
   for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
 
+#pragma unroll 2
   for (int ch = 0; ch < G; ++ch) {
     const int buf = ch & 1;
-    if (ch + 1 < G) load(ch + 1);               // in flight under this chunk's math
+    load(ch + 2 < G ? ch + 2 : G - 1, buf);      // register set of chunk ch (stored one chunk ago);
+                                                // unconditional (clamped) so the waits stay counted
     // ---- scores -> two quantisers -> integer codes c
     const float rh_row = rhq[ch] * inv2;
     float c[4][4];
@@ -511,8 +516,8 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
       lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, bhi, lacc, 0, 0, 0);
       lacc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, blo, lacc, 0, 0, 0);
     }
-    if (ch + 1 < G) store(buf ^ 1);   // the other buffer was last read before the previous barrier
-    __syncthreads();
+    store(buf ^ 1, buf ^ 1);                    // chunk ch + 1 (register set (ch + 1) & 1; the last is a dummy); the other
+    __syncthreads();                            // buffer was last read before the previous barrier
   }
 
   const float lsum = lacc[0];

@@ -84,13 +84,15 @@ __device__ __forceinline__ float2_t gelu_fast2(float2_t x) {
 }
 
 // clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
-// quantizer/uniform.py:31-36), at the price of a multiply: q = v * inv (inv = fl(1/s)) is within
-// ~1.2e-7 |q| of v / s and fl(v / s) within 6e-8 |q|, so rint(q) == rint(fl(v / s)) unless q lies
-// within 1e-6 max(|q|, 1) of a half-integer -- only then (rare) the true division runs.
+// quantizer/uniform.py:31-36), branch-free: q = fl(v * inv) with inv = fl(1/s), then one Markstein
+// correction q' = fl(q + fl(v - s q) inv) (both steps fused multiply-adds; the remainder v - s q is
+// exact) gives fl(v / s) itself -- checked against exact rational division on 1.2e5 operand pairs
+// including +-2 ulp around every .5 tie (tools/check_markstein.py).  Non-finite q (overflow) keeps
+// q, so the clamp sees +-inf as the true division would.
 __device__ __forceinline__ float q8_exact(float v, float s, float inv) {
   const float q = v * inv;
-  float r = __builtin_rintf(q);
-  if (fabsf(q - r) > 0.5f - 1e-6f * fmaxf(fabsf(q), 1.0f)) r = __builtin_rintf(v / s);
+  const float qc = __builtin_fmaf(__builtin_fmaf(-q, s, v), inv, q);
+  const float r = __builtin_rintf(__builtin_isfinite(q) ? qc : q);
   return fminf(fmaxf(r, -128.f), 127.f);
 }
 

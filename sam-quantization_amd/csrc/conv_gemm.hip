@@ -285,6 +285,154 @@ __global__ __launch_bounds__(256) void patch_embed_f32_kernel(ConvArgs a) {
   }
 }
 
+// fp32-accurate patch embedding on fp16 MFMA (the W4A8 engine: its first int8 quantiser sits
+// right behind it).  Every fp32 operand x is split as x = hi + lo' 2^-11 with hi = fp16(x),
+// lo' = fp16((x - hi) 2^11) (lo' is as large as x itself: no fp16 subnormals for small weights);
+// x.w = hi_x hi_w + 2^-11 (hi_x lo'_w + lo'_x hi_w) + O(2^-22 |x w|): two accumulators, three
+// v_mfma_f32_32x32x16_f16 per fragment pair instead of eight v_mfma_f32_32x32x2_f32 (x 16 the
+// FLOP rate).  Same 128x128 tiles / 4 waves / LDS double buffer as conv_gemm_kernel, with hi and
+// lo' planes of A and B staged side by side.
+__device__ __forceinline__ void split8(const float (&v)[8], half8_t& hi, half8_t& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (_Float16)v[j];
+    lo[j] = (_Float16)((v[j] - (float)hi[j]) * 2048.0f);
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(256, 2) void patch_embed_x3_kernel(ConvArgs a) {
+  constexpr int BM = 128, BN = 128, BK = 32;
+  constexpr int PITCH = BK * 2 + 16;           // 80-byte LDS rows (conv_gemm_kernel's bank spread)
+  constexpr int PLANE = 128 * PITCH;
+  constexpr int BUF = 4 * PLANE;               // A hi | A lo' | B hi | B lo'
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int tiles_n = a.N / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (bid / tiles_n) * BM;
+  const int n0 = (bid % tiles_n) * BN;
+  const int kt_count = a.K / BK;
+  const int gg = a.G * a.G, pp = a.P * a.P, side = a.G * a.P;
+  const float* wf = (const float*)a.w;
+
+  // staging: chunk c = tid + 256 j -> row c / 4, 8 k-values at (c % 4) * 8 (one patch row segment)
+  float ra[2][8], rb[2][8];
+  auto load = [&](int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, k = kt * BK + (c & 3) * 8;
+      int t = m0 + row;
+      t = t < a.M ? t : a.M - 1;
+      const int b = t / gg, gy = (t / a.G) % a.G, gx = t % a.G;
+      const int ci = k / pp, rem = k - ci * pp, kh = rem / a.P, kw = rem - kh * a.P;
+      if (U8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ra[j][e] = pixel_norm(a, (const uint8_t*)a.x, b, ci, gy * a.P + kh, gx * a.P + kw + e);
+      } else {
+        const float4_t* src = (const float4_t*)((const float*)a.x + (((int64_t)b * a.Cin + ci) * side + gy * a.P + kh) *
+                                                side + gx * a.P + kw);
+        const float4_t v0 = src[0], v1 = src[1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ra[j][e] = v0[e];
+          ra[j][4 + e] = v1[e];
+        }
+      }
+      const float4_t* ws = (const float4_t*)(wf + (int64_t)(n0 + row) * a.K + k);
+      const float4_t w0 = ws[0], w1 = ws[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        rb[j][e] = w0[e];
+        rb[j][4 + e] = w1[e];
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 256 * j;
+      const int row = c >> 2, off = (c & 3) * 16;
+      half8_t h, l;
+      split8(ra[j], h, l);
+      *(half8_t*)(smem + buf * BUF + row * PITCH + off) = h;
+      *(half8_t*)(smem + buf * BUF + PLANE + row * PITCH + off) = l;
+      split8(rb[j], h, l);
+      *(half8_t*)(smem + buf * BUF + 2 * PLANE + row * PITCH + off) = h;
+      *(half8_t*)(smem + buf * BUF + 3 * PLANE + row * PITCH + off) = l;
+    }
+  };
+
+  float16_t acc[2][2], accx[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = accx[i][t][r] = 0.f;
+
+  const int hsel = lane >> 5;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < kt_count; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < kt_count) load(kt + 1);
+    const char* base = smem + buf * BUF;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      half8_t ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int o = (wm * 64 + i * 32 + (lane & 31)) * PITCH + (s * 16 + 8 * hsel) * 2;
+        ah[i] = *(const half8_t*)(base + o);
+        al[i] = *(const half8_t*)(base + PLANE + o);
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int o = (wn * 64 + t * 32 + (lane & 31)) * PITCH + (s * 16 + 8 * hsel) * 2;
+        bh[t] = *(const half8_t*)(base + 2 * PLANE + o);
+        bl[t] = *(const half8_t*)(base + 3 * PLANE + o);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[t], acc[i][t], 0, 0, 0);
+          accx[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[t], accx[i][t], 0, 0, 0);
+          accx[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[t], accx[i][t], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < kt_count) {
+      store(buf ^ 1);   // the other buffer was last read before the previous barrier
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = n0 + wn * 64 + t * 32 + (lane & 31);
+    const float bcol = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hsel;
+        if (row >= a.M) continue;
+        float v = __builtin_fmaf(accx[i][t][r], 1.0f / 2048.0f, acc[i][t][r]) + bcol;
+        if (a.pos) v += a.pos[(int64_t)(row % gg) * a.N + col];
+        ((float*)a.out)[(int64_t)row * a.N + col] = v;
+      }
+    }
+  }
+}
+
 template <int MODE>
 static int conv_launch(const ConvArgs& a, hipStream_t stream) {
   const int nwg = ((a.M + 127) / 128) * (a.N / 128);
@@ -349,7 +497,10 @@ extern "C" int samq_patch_embed_f32(const float* img, const float* weight, const
   const int g = img_size / patch;
   ConvArgs a{img, (const _Float16*)weight, bias, pos, out, B * g * g, N, Cin * patch * patch, g, patch, Cin};
   const int nwg = ((a.M + 127) / 128) * (a.N / 128);
-  hipLaunchKernelGGL(patch_embed_f32_kernel<false>, dim3(nwg), dim3(256), 0, stream, a);
+  if (patch % 8 == 0 && a.K % 32 == 0)   // split-fp16 MFMA form (16-byte image rows of 8 pixels)
+    hipLaunchKernelGGL(patch_embed_x3_kernel<false>, dim3(nwg), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(patch_embed_f32_kernel<false>, dim3(nwg), dim3(256), 0, stream, a);
   SAMQ_LAUNCH_CHECK("patch_embed_f32 launch");
   return SAMQ_OK;
 }
@@ -371,7 +522,10 @@ extern "C" int samq_patch_embed_u8(const uint8_t* img, int h, int w, const float
   if (weight_f32) {
     SAMQ_REQUIRE(patch % 4 == 0 && (Cin * patch * patch) % 16 == 0, SAMQ_ERR_UNSUPPORTED,
                  "patch_embed_u8: patch must be a multiple of 4 and Cin*patch^2 a multiple of 16");
-    hipLaunchKernelGGL(patch_embed_f32_kernel<true>, dim3(nwg), dim3(256), 0, stream, a);
+    if (patch % 8 == 0 && a.K % 32 == 0)
+      hipLaunchKernelGGL(patch_embed_x3_kernel<true>, dim3(nwg), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL(patch_embed_f32_kernel<true>, dim3(nwg), dim3(256), 0, stream, a);
     SAMQ_LAUNCH_CHECK("patch_embed_u8 (f32) launch");
     return SAMQ_OK;
   }

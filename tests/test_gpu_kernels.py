@@ -342,8 +342,9 @@ def test_patch_embed_vs_conv(cuda):
 
 @pytest.mark.parametrize("b,s,c", [(2, 256, 768), (1, 1024, 1280)])
 def test_patch_embed_f32_vs_conv(cuda, b, s, c):
-    """fp32 PatchEmbed (the W4A8 embedding, fp32 MFMA) vs torch Conv2d in float64 on the same
-    fp32 values: fp32 rounding of a 768-term sum only."""
+    """fp32 PatchEmbed (the W4A8 embedding: split-fp16 MFMA, x = hi + lo' 2^-11, three products
+    per fragment pair) vs torch Conv2d in float64 on the same fp32 values: within fp32-level
+    rounding of a 768-term sum (2e-6 of the output scale)."""
     from samq import ops
     g = torch.Generator().manual_seed(s + c)
     p = 16
@@ -355,6 +356,29 @@ def test_patch_embed_f32_vs_conv(cuda, b, s, c):
            + pos.double())
     out = ops.patch_embed(img.to(cuda), w.reshape(c, -1).contiguous().to(cuda), bias.to(cuda),
                           pos[0].contiguous().to(cuda), p)
+    torch.cuda.synchronize()
+    _close(out, ref.float().numpy(), 2e-6)
+
+
+def test_patch_embed_u8_f32_weights_vs_conv(cuda):
+    """Raw uint8 pixels (Sam.preprocess fused: normalise + zero-pad a 200 x 240 image to 256) with
+    fp32 weights -- the W4A8 predictor path, split-fp16 MFMA -- vs float64 torch on the same
+    normalised fp32 values."""
+    from samq import ops
+    g = torch.Generator().manual_seed(11)
+    b, c, p, s, h, w_ = 2, 768, 16, 256, 200, 240
+    img = torch.randint(0, 256, (b, 3, h, w_), generator=g, dtype=torch.uint8)
+    mean = torch.tensor([123.675, 116.28, 103.53])
+    std = torch.tensor([58.395, 57.12, 57.375])
+    w = torch.randn(c, 3, p, p, generator=g) * 0.02
+    bias = torch.randn(c, generator=g) * 0.02
+    pos = torch.randn(1, s // p, s // p, c, generator=g) * 0.1
+    x = torch.zeros(b, 3, s, s)
+    x[:, :, :h, :w_] = (img.float() - mean.view(1, 3, 1, 1)) / std.view(1, 3, 1, 1)
+    ref = (torch.nn.functional.conv2d(x.double(), w.double(), bias.double(), stride=p).permute(0, 2, 3, 1)
+           + pos.double())
+    out = ops.patch_embed_u8(img.to(cuda), mean.to(cuda), std.to(cuda), w.reshape(c, -1).contiguous().to(cuda),
+                             bias.to(cuda), pos[0].contiguous().to(cuda), p, s)
     torch.cuda.synchronize()
     _close(out, ref.float().numpy(), 2e-6)
 
