@@ -360,8 +360,7 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
         }
         mx = fmaxf(mx, my);
       }
-      mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = max_rows4(mx);
       const float th = th_w[(t * TH_ROWS + kh) * 16 + ql];
       // lazy rescale: the exp2 offset m only moves when the row max exceeds it by > 8 (P <= 2^8,
       // far inside fp16; O and l carry the same offset, so O / l is unchanged) -- most key rows
@@ -723,8 +722,7 @@ struct Win {
         my = max3f(my, sc[t][kh + 1][2], sc[t][kh + 1][3]);
       }
       mx = fmaxf(mx, my);
-      mx = max3f(mx, __shfl_xor(mx, 16, 64), __shfl_xor(mx, 32, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = max_rows4(mx);
 #pragma unroll
       for (int pr = 0; pr < S / 2; ++pr)
 #pragma unroll
@@ -1039,7 +1037,12 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       my = max3f(my, sc[1][r], sc[1][r + 1]);
     }
     mx = max3f(mx, my, fmaxf(sc[0][15], sc[1][15]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    {   // lane ^ 32 (the query's other 32 keys): one VALU permlane swap instead of an LDS bpermute
+        // (v_permlane32_swap of mx with itself: result 0 holds mx[l & 31], result 1 mx[32 + (l & 31)])
+      const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, mx), __builtin_bit_cast(int, mx),
+                                                       false, false);
+      mx = fmaxf(__builtin_bit_cast(float, (int)sw[0]), __builtin_bit_cast(float, (int)sw[1]));
+    }
     const float mrow = mx + th_cur;
     const bool unsafe = !(mrow <= m + 15.0f);   // (m = -inf: unsafe)
     if (__any(unsafe)) {

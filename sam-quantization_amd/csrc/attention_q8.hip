@@ -240,8 +240,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
         cmax = fmaxf(cmax, c);
       }
     }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    cmax = max_rows4(cmax);
     if (cmax > m) {
       const float alpha = m == -INFINITY ? 0.f : exp2f((m - cmax) * p.k2);
       lsum *= alpha;
@@ -481,8 +480,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
     cmax = q8max3(cmax, c[2][3], c[3][0]);
     cmax = q8max3(cmax, c[3][1], c[3][2]);
     cmax = fmaxf(cmax, c[3][3]);
-    cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = max_rows4(cmax);
     if (cmax > m + lazy) {   // per query column: move the offset, rescale O and l
       const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
 #pragma unroll
@@ -679,8 +677,7 @@ __global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_wi
     cmax = q8max3(cmax, c[2][3], c[3][0]);
     cmax = q8max3(cmax, c[3][1], c[3][2]);
     cmax = fmaxf(cmax, c[3][3]);
-    cmax = q8max3(cmax, __shfl_xor(cmax, 16, 64), __shfl_xor(cmax, 32, 64));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = max_rows4(cmax);
     if (cmax > m + lazy) {
       const float alpha = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f((m - cmax) * k2);
 #pragma unroll

@@ -96,6 +96,16 @@ __device__ __forceinline__ float q8_exact(float v, float s, float inv) {
   return fminf(fmaxf(r, -128.f), 127.f);
 }
 
+// max over the four 16-lane rows of a wave at the same column (lane ^ 16, ^ 32, ^ 48): two VALU
+// permlane swaps (v_permlane16_swap / v_permlane32_swap of a value with itself: results 0 / 1 hold
+// the row pair's two values) instead of three LDS bpermutes
+__device__ __forceinline__ float max_rows4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v), false, false);
+  v = fmaxf(__builtin_bit_cast(float, (int)a[0]), __builtin_bit_cast(float, (int)a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v), false, false);
+  return fmaxf(__builtin_bit_cast(float, (int)b[0]), __builtin_bit_cast(float, (int)b[1]));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

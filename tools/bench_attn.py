@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--heads", type=int, default=16)
     ap.add_argument("--hd", type=int, default=80)
     ap.add_argument("--window-only", action="store_true")
+    ap.add_argument("--global-only", action="store_true")
     ap.add_argument("--q8", action="store_true", help="int8 output codes (the W4A8 proj-input QAct store)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -27,7 +28,7 @@ def main():
     c = heads * d
     qkv = (torch.randn(b, g, g, 3 * c, device=dev) * 0.5).half()
     bias = (torch.randn(3 * c, device=dev) * 0.1).half()
-    for window in ((14,) if args.window_only else (14, 0)):
+    for window in ((14,) if args.window_only else (0,) if args.global_only else (14, 0)):
         side = window or g
         rh = (torch.randn(2 * side - 1, d, device=dev) * 0.1).half()
         rw = (torch.randn(2 * side - 1, d, device=dev) * 0.1).half()
