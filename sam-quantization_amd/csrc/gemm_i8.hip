@@ -518,10 +518,15 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
       // ---------------- load half
       if (p == NPH - 1 && kt + 1 < kt_count) {
         // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
-        int newer = pf ? PRE_LAST : 0;
+        // (steady state: a compile-time count instead of the runtime SALU decision tree)
+        if (pf && kt + LA < kt_count) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"((LA - 2) * NPW + PRE_LAST) : "memory");
+        } else {
+          int newer = pf ? PRE_LAST : 0;
 #pragma unroll
-        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
-        i8_vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+          for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? NPW : 0;
+          i8_vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+        }
       }
       u32x4 bw[TN];
 #pragma unroll

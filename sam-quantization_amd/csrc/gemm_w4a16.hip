@@ -1407,11 +1407,17 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     for (int p = 0; p < NPH; ++p) {
       // ---------------- load half
       if (p == NPH - 1 && kt + 1 < kt_count) {
-        // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
-        int newer = pf ? PRE_LAST : 0;
+        // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far.
+        // Per-channel steady state (every later tile whole, restaging on): a compile-time count --
+        // the runtime form is a ~40-SALU / 15-branch decision tree on the load half's stream
+        if (!GR && pf && kt + LA < kt_count) {
+          vm_wait<(LA - 2) * NPW + PRE_LAST>();
+        } else {
+          int newer = pf ? PRE_LAST : 0;
 #pragma unroll
-        for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? npieces(kt + j) : 0;
-        vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+          for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? npieces(kt + j) : 0;
+          vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+        }
       }
       if (GR && !G_NOROW && p == 0 && gk == 0) {   // first K tile of a group: its scale / zero splats
 #pragma unroll
