@@ -426,6 +426,8 @@ def main():
                     help="image groups run as concurrent kernel chains on separate HIP streams "
                          "(0 = 2 when the per-GPU batch is even, else 1; W8A8 runs one chain)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lane-stagger", type=int, default=None,
+                    help="W4A16 lanes: lane i+1 waits for lane i's launch k (7 per block; -1 = none; default: the engine's 1)")
     ap.add_argument("--fold-ln", action="store_true",
                     help="W4A16: fold the LayerNorms into the GEMM epilogues (opt-in A/B; measured slower)")
     ap.add_argument("--no-isolated", action="store_true",
@@ -485,6 +487,8 @@ def main():
     eng = enc.engine()
     if args.fold_ln:
         eng.fold_ln = True
+    if args.lane_stagger is not None:
+        eng.lane_stagger = args.lane_stagger
     log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB "
         f"in {t_bc * 1e3:.1f} ms)")
 

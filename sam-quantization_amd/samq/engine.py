@@ -52,6 +52,9 @@ class EncoderEngine:
         # 2-lane bench graph the fold epilogues cost more than the two LayerNorm launches they
         # replace (isolated per block 358 vs 351 us, step 23.4 vs 23.0 ms)
         self.fold_ln = False
+        # lanes > 1: lane i+1 starts after lane i's launch number ``lane_stagger`` (7 per block,
+        # block 0 first; -1 = all lanes start together) -- an in-graph A/B knob
+        self.lane_stagger = 1   # measured: +0.3 % over no stagger (profiles/r3_v9_lane_stagger.log)
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
@@ -241,17 +244,26 @@ class EncoderEngine:
         else:
             p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
 
-    def block(self, p: _BlockPlan, bufs) -> None:
+    def block(self, p: _BlockPlan, bufs, mark=None) -> None:
+        """One W4A16 block (7 launches).  ``mark(k)`` (lane stagger) runs after launch k."""
         if self.w4a8:
             return self.block_w4a8(p, bufs)
+        mark = mark or (lambda k: None)
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
         ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw)
+        mark(0)
         p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
+        mark(1)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        mark(2)
         p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
+        mark(3)
         ops.layernorm(x, p.ln2_w, p.ln2_b, p.ln2_eps, out=xn, rows_per_wave=self.ln_rpw)
+        mark(4)
         p.lin1.forward_epilogue(xn, ops.EPI_BIAS_GELU, out=hid)
+        mark(5)
         p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
+        mark(6)
 
     def neck(self, x32: torch.Tensor, out_dtype) -> torch.Tensor:
         """Neck (image_encoder.py:88-104) on NHWC tokens: 1x1 conv (HIP, fp32 tokens -> fp16),
@@ -298,9 +310,14 @@ class EncoderEngine:
         for s in streams:
             s.wait_stream(cur)
         outs = []
+        gate = None   # lane stagger: lane i starts once lane i-1 has issued its first launches
         for i, s in enumerate(streams):
             with torch.cuda.stream(s):
-                outs.append(self._forward(img[i * bl:(i + 1) * bl], self.buffers(bl, i), out_dtype))
+                if gate is not None:
+                    s.wait_event(gate)
+                ev = torch.cuda.Event() if self.lane_stagger >= 0 and i + 1 < lanes else None
+                outs.append(self._forward(img[i * bl:(i + 1) * bl], self.buffers(bl, i), out_dtype, ev))
+                gate = ev
         n, c, h, w = outs[0].shape
         out = torch.empty((b, h, w, c), dtype=out_dtype, device=img.device).permute(0, 3, 1, 2)
         for i, s in enumerate(streams):  # nothing was enqueued on ``cur`` since the fork
@@ -315,14 +332,24 @@ class EncoderEngine:
             ss = self._streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
         return ss[:lanes]
 
-    def _forward(self, img: torch.Tensor, bufs, out_dtype) -> torch.Tensor:
+    def _forward(self, img: torch.Tensor, bufs, out_dtype, gate_event=None) -> torch.Tensor:
         self.embed(img, bufs["x"])
         if self._fold_ready and self._fold_usable(bufs["x"].numel() // self.C):
             for i in range(len(self.plans)):
                 self.block_fold(i, bufs)
+            if gate_event is not None:
+                gate_event.record()
         else:
-            for p in self.plans:
-                self.block(p, bufs)
+            for i, p in enumerate(self.plans):
+                mark = None
+                if gate_event is not None and i == self.lane_stagger // 7:
+                    k0 = self.lane_stagger % 7
+                    mark = lambda k, k0=k0: gate_event.record() if k == k0 else None  # noqa: E731
+                self.block(p, bufs, mark)
+                if mark is not None and self.w4a8:   # the W4A8 block takes no marks: gate after it
+                    gate_event.record()
+            if gate_event is not None and self.lane_stagger // 7 >= len(self.plans):
+                gate_event.record()
         return self.neck(bufs["x"], out_dtype)
 
     __call__ = forward
