@@ -29,4 +29,7 @@ run instep88 500 bash tools/instep_profile.sh w8a8
 run instepb8 500 bash tools/instep_profile.sh w4a16 --batch 8
 run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128
 run pmc 900 bash tools/pmc_all.sh
+# keep the summaries only (gpurun copies back at most 64 MiB of gpurun_out/)
+rm -rf gpurun_out/instep_*_/ gpurun_out/pmc_*_fetch gpurun_out/pmc_*_write
+du -sh gpurun_out
 exit 0
