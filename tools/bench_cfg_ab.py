@@ -22,7 +22,8 @@ if len(sys.argv) > 3:   # variants as "name:layer=cfg,layer=cfg;name:..." (pick 
         name, spec = v.split(":")
         VARIANTS[name] = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in spec.split(",")}
 
-enc = random_quant_encoder("vit_h", -1, device=dev)
+import os  # noqa: E402
+enc = random_quant_encoder("vit_h", int(os.environ.get("SAMQ_AB_GS", "-1")), device=dev)   # groupsize
 eng = enc.engine()
 g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((4, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
