@@ -69,8 +69,11 @@ class QuantLlamaMLP(nn.Module):
         self.down_proj = down_proj
 
     def gated_operands(self):
-        """The interleaved gate/up operands of the fused kernel, built once per device."""
-        key = self.gate_proj_qweight.device
+        """The interleaved gate/up operands of the fused kernel, built once and rebuilt when any of
+        the six packed buffers moves or is written (data pointer / in-place version counter)."""
+        bufs = (self.gate_proj_qweight, self.gate_proj_scales, self.gate_proj_qzeros, self.up_proj_qweight,
+                self.up_proj_scales, self.up_proj_qzeros)
+        key = tuple((b.data_ptr(), b._version) for b in bufs)
         if getattr(self, "_gated", None) is None or self._gated[0] != key:
             self._gated = (key, _gated_operands(self.gate_proj_qweight, self.gate_proj_scales, self.gate_proj_qzeros,
                                                 self.up_proj_qweight, self.up_proj_scales, self.up_proj_qzeros))

@@ -100,3 +100,6 @@ def test_gated_mlp_one_launch_matches_two_gemms_and_module(cuda):
     assert y.shape == (2, m // 2, k)
     assert (y.float() - y_ref.float()).abs().max().item() <= 5e-3 * max(1.0, y_ref.float().abs().max().item())
     assert mlp._gated is not None and mlp(a.view(2, m // 2, k)).equal(y)
+    mlp.up_proj_scales.mul_(2)            # in-place weight update: the cached operands are rebuilt
+    y2 = mlp(a.view(2, m // 2, k))
+    assert (y2.float() - 2 * y.float()).abs().max().item() <= 1e-2 * max(1.0, y.float().abs().max().item())
