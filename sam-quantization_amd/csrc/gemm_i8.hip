@@ -624,7 +624,8 @@ static int launch_i8_pp2(const I8Args& a, hipStream_t st) {
   return SAMQ_OK;
 }
 
-// tile configs: 81 256x256 (W4: 3 stages; W8: 2), 82 128x256, 83 128x128, 84 64x64;
+// tile configs: 81 256x256 (W4: 3 stages; W8: 2), 82 128x256, 83 128x128, 84 64x64, 87 128x64,
+// 88 64x128, 89 64x64 on 2 stages;
 // 85 the W4 ping-pong kernel (256x256, 3-slot ring, lookahead 2)
 template <int EPI, int BF>
 static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
@@ -650,12 +651,19 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 82: return launch_i8<128, 256, 2, 4, EPI, BF, 3>(a, st);
     case 83: return launch_i8<128, 128, 2, 2, EPI, BF, 3>(a, st);
     case 84: return launch_i8<64, 64, 2, 2, EPI, BF, 3>(a, st);
+    case 87: return launch_i8<128, 64, 2, 2, EPI, BF, 3>(a, st);
+    case 88: return launch_i8<64, 128, 2, 2, EPI, BF, 3>(a, st);
+    case 89: return launch_i8<64, 64, 2, 2, EPI, BF, 2>(a, st);
+    case 90: return launch_i8<64, 128, 2, 2, EPI, BF, 2>(a, st);
+    case 91: return launch_i8<32, 64, 1, 2, EPI, BF, 2>(a, st);
+    case 92: return launch_i8<64, 32, 2, 1, EPI, BF, 2>(a, st);
     default: return fail(SAMQ_ERR_INVALID, "i8_gemm: unknown tile config");
   }
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 95: case 96: case 97: return 256; case 83: return 128; case 84: return 64; default: return 0; }
+  switch (cfg) { case 81: case 82: case 85: case 86: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
+    case 92: return 32; default: return 0; }
 }
 
 static int i8_pick_cfg(int M, int N, int bfmt) {
@@ -676,7 +684,10 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
   const int64_t t256 = (int64_t)((M + 127) / 128) * (N / 256);
   // W8 below two rounds of 128x256 tiles (fq_vit vit_b at B=1, M = 4096): 64x64 tiles fill the
   // chip — per block 77 vs 88-90 us (tools/bench_i8.py --w8-vitb, profiles/r1_v17_w8_scan.log).
-  if (bfmt == BF_W8 && t256 < 512 && N % 64 == 0) return 84;
+  // Round 3: on a 2-stage ring (32 KiB LDS, five workgroups per CU instead of three) the W8A8
+  // graph takes 1.8325 vs 1.8610 ms per image, bit-identical; 128x64 / 64x128 tiles were slower
+  // (tools/bench_cfg_ab_w8a8.py, profiles/r3_w8_cfg_ab.log).
+  if (bfmt == BF_W8 && t256 < 512 && N % 64 == 0) return 89;
   if (N % 256 == 0 && t256 >= 512) return 82;
   if (N % 128 == 0 && M >= 256) return 83;
   return 84;

@@ -753,11 +753,12 @@ class W8A8Engine:
         # round(fp32(w / s)) with the correctly rounded fp32 quotient (uniform.py:31-36)
         codes = torch.clamp(torch.round((w2.double() / s.double()[:, None]).float()), -128, 127).to(torch.int8)
         bias = None if mod.bias is None else mod.bias.detach().float().contiguous()
-        return dict(packed=self.ops.w8_repack(codes), scale=s.contiguous(), bias=bias, n=n, k=w2.shape[1])
+        return dict(packed=self.ops.w8_repack(codes), scale=s.contiguous(), bias=bias, n=n, k=w2.shape[1],
+                    cfg=0)   # i8 GEMM tile config (0: the library's pick)
 
     def _gemm(self, a, lw, epi, a_scale, out_scale, mid=0.0, res=None, res_scale=0.0, out=None):
         return self.ops.w8a8_gemm(a, lw["packed"], lw["scale"], lw["n"], lw["bias"], epi, a_scale, out_scale, mid,
-                                  res_scale, res, out)
+                                  res_scale, res, out, cfg=lw["cfg"])
 
     @torch.no_grad()
     def forward(self, img: torch.Tensor, taps: Optional[dict] = None) -> torch.Tensor:

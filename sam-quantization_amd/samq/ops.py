@@ -396,10 +396,10 @@ def i8_gemm(a: torch.Tensor, bfmt: int, wpacked: torch.Tensor, wscale: torch.Ten
 
 
 def w8a8_gemm(a, wpacked, wscale, n, bias=None, epilogue=EPI_Q8, a_scale=1.0, out_scale=0.0, mid_scale=0.0,
-              res_scale=0.0, res=None, out=None):
+              res_scale=0.0, res=None, out=None, cfg=0):
     """fq_vit QLinear on int8 codes: ``epilogue(float(sum a w) * a_scale * wscale[n] + bias[n])``."""
     return i8_gemm(a, _lib.BF_W8, wpacked, wscale, n, bias, None, epilogue, a_scale, out_scale, mid_scale,
-                   res_scale, res, out)
+                   res_scale, res, out, cfg)
 
 
 def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: torch.Tensor, n: int,

@@ -83,7 +83,7 @@ def _rq(v, s):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 84])
+@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 84, 87, 88, 89, 90, 91, 92])
 def test_w8a8_gemm_epilogues(cuda, cfg):
     from samq import ops
     rng = np.random.Generator(np.random.PCG64(11 + cfg))
