@@ -275,9 +275,35 @@ def gemm_flops_per_step(mode, eng, images):
                for p in eng.plans for lin in (p.qkv, p.proj, p.lin1, p.lin2))
 
 
-def cpu_baseline(model_name: str, mode: str = "w4a16"):
+def oracle_state(enc, cfg, groupsize: int):
+    """The bench encoder's own weights in the oracle's (reference) naming: non-Linear parameters
+    as fp32 tensors of their fp16 values, every block Linear dequantised from its packed GPTQ
+    buffers in G1 semantics (s * (q - zp), oracle/gptq_pack.dequant_g1) -- the checkpoint the
+    reference would load (gptq4sam_infer.py:135-141 load_quant)."""
+    import numpy as np
+    from oracle import sam_ref, synth
+    sd = {}
+    for k, v in enc.state_dict().items():
+        sd[k.replace("attn.qkv_proj.", "attn.qkv.").replace("attn.o_proj.", "attn.proj.")] = v.detach().cpu()
+    names = synth.linear_names(cfg)
+    q = {}
+    for n in names:
+        q[n + ".qweight"] = sd[n + ".qweight"].numpy()
+        q[n + ".qzeros"] = sd[n + ".qzeros"].numpy()
+        q[n + ".scales"] = sd[n + ".scales"].numpy()
+    lw = sam_ref.quantized_linear_weights(q, names, groupsize)
+    lb = {n: sd[n + ".bias"].float().numpy() for n in names}
+    lin = tuple(n + "." for n in names)
+    st = {k: v.half().float().numpy() for k, v in sd.items() if not k.startswith(lin) and v.is_floating_point()}
+    return st, lw, lb, np
+
+
+def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, groupsize: int = -1):
     """Oracle restatement of the reference CPU fake-quant path (fp32 encoder with dequantised
-    int4 weights), one 1024x1024 image, rank 0 only."""
+    int4 weights), one 1024x1024 image, rank 0 only.  W4A16 / W4A8: the oracle is built from the
+    bench encoder's own packed weights (``enc``) and runs the bench's image 0 (``img0``), so its
+    output doubles as the parity reference (returned second; None for W8A8, whose baseline runs
+    the fq_vit op graph on seeded random weights)."""
     sys.path.insert(0, str(REPO))
     from oracle import sam_ref, synth
     threads = len(os.sched_getaffinity(0))
@@ -286,8 +312,11 @@ def cpu_baseline(model_name: str, mode: str = "w4a16"):
     cfg = synth.encoder_config(model_name)
     g = torch.Generator().manual_seed(0)
     st = {}
-    for k, shape in _state_shapes(cfg).items():
-        st[k] = torch.randn(shape, generator=g) * 0.02
+    if enc is None or mode == "w8a8":
+        for k, shape in _state_shapes(cfg).items():
+            st[k] = torch.randn(shape, generator=g) * 0.02
+    else:
+        st, lw, lb, _ = oracle_state(enc, cfg, groupsize)
     if mode == "w8a8":
         from oracle import fq_ref
         o = fq_ref.FQEncoderOracle(cfg, st)
@@ -300,23 +329,33 @@ def cpu_baseline(model_name: str, mode: str = "w4a16"):
         what = "fq_vit W8A8 fake-quant op graph (oracle/fq_ref.py)"
     elif mode == "w4a8":
         from oracle import w4a8_ref
-        o = w4a8_ref.W4A8EncoderOracle(cfg, st)
-        o.set_scales({n: 0.05 for n in synth.linear_names(cfg)})
+        if enc is None:
+            o = w4a8_ref.W4A8EncoderOracle(cfg, st)
+            o.set_scales({n: 0.05 for n in synth.linear_names(cfg)})
+        else:
+            from samq import QuantLinear
+            o = w4a8_ref.W4A8EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb)
+            o.set_scales({n.replace("qkv_proj", "qkv").replace("o_proj", "proj"): float(m.act_quant.quantizer.scale)
+                          for n, m in enc.named_modules() if isinstance(m, QuantLinear)})
         what = "W4A8 fake-quant op graph (oracle/w4a8_ref.py)"
     else:
-        o = sam_ref.EncoderOracle(cfg, st)
+        o = sam_ref.EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb) if enc is not None else \
+            sam_ref.EncoderOracle(cfg, st)
         what = "fp32 CPU fake-quant op graph (oracle/sam_ref.py)"
-    img = torch.randn(1, 3, 1024, 1024, generator=g)
+    own = enc is not None and mode != "w8a8" and img0 is not None
+    img = img0.detach().float().cpu().reshape(1, 3, 1024, 1024) if own else torch.randn(1, 3, 1024, 1024, generator=g)
     o(img)   # warm-up (allocator, thread pool)
     runs = []
     for _ in range(3):
         t0 = time.perf_counter()
-        o(img)
+        ref = o(img)
         runs.append(time.perf_counter() - t0)
     dt = statistics.median(runs)
+    src = "the bench encoder's own packed weights and image 0" if own else "seeded random weights"
     return dict(value=round(1.0 / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample=f"1 image, {model_name} {what}; median of 3 runs after 1 warm-up "
-                       f"({', '.join(f'{r:.2f}' for r in runs)} s), torch {threads} threads, CPU: {_cpu_model()}")
+                sample=f"1 image, {model_name} {what} on {src}; median of 3 runs after 1 warm-up "
+                       f"({', '.join(f'{r:.2f}' for r in runs)} s), torch {threads} threads, CPU: {_cpu_model()}"
+                ), (ref if own else None)
 
 
 def _state_shapes(cfg):
@@ -472,14 +511,15 @@ def main():
         enc = random_fq_encoder(model, device=dev)
         nbytes = 0
     else:
-        enc = random_quant_encoder(model, args.groupsize, device=dev, init=(rank == 0))
+        # model.half() as the reference's entry point runs it (gptq4sam_infer.py:59-79): the fp16
+        # parameter values are what the engine and the parity oracle both see
+        enc = random_quant_encoder(model, args.groupsize, device=dev, init=(rank == 0)).half()
         torch.cuda.synchronize()
         tb = time.perf_counter()
         nbytes = sdist.broadcast_state(enc, src=0)
         torch.cuda.synchronize()
         t_bc = time.perf_counter() - tb
         if mode == "w4a8":
-            enc.half()
             samq.make_act_quant(enc)
             gcal = torch.Generator(device="cpu").manual_seed(99)
             cal = torch.randn((1, 3, 1024, 1024), generator=gcal).to(dev, torch.float16)
@@ -594,8 +634,23 @@ def main():
                      "broadcast_bytes": nbytes, "broadcast_ms": round(t_bc * 1e3, 2),
                      "rank0_shard": [start, stop]},
         }
+        line["parity"] = None
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(model, mode)
+            line["cpu_baseline"], ref = cpu_baseline(model, mode, enc, img[0], args.groupsize)
+            if ref is not None:
+                # the north star's "encoder-output max-abs-diff": the engine on image 0 (outside
+                # the timed region) vs the oracle fed the same weights and image
+                with torch.no_grad():
+                    mine = eng(img[:1], out_dtype=torch.float32).float().cpu()
+                d = (mine - ref.float()).abs()
+                line["parity"] = {
+                    "oracle": {"w4a16": "G1 (oracle/sam_ref.py: fp32 encoder, GPTQ weights s*(q-zp))",
+                               "w4a8": "W4A8 composition (oracle/w4a8_ref.py) with the engine's calibrated "
+                                       "activation scales"}[mode],
+                    "image": 0, "max_abs_vs_oracle": float(d.max()), "mean_abs": float(d.mean()),
+                    "ref_absmax": float(ref.abs().max()),
+                    "tolerance": 1e-2 if mode == "w4a16" else None,
+                    "pass": bool(float(d.max()) <= 1e-2) if mode == "w4a16" else None}
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -110,7 +110,9 @@ int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, cons
 #define SAMQ_EPI_SILU_MUL 10   /* internal: the samq_w4a16_gated_mlp epilogue */
 /* samq_w4a16_gemm_cfg with the LayerNorm-fold epilogues above (ping-pong configs 57 / 64 / 0 =
  * automatic at M >= 8192 only, else SAMQ_ERR_UNSUPPORTED): gamma f32 [N] (producer), gw / bw f32
- * [N] (consumer), stats f32, mu f32 [M], aout f16 [M,N] (producer), eps of the folded LayerNorm. */
+ * [N] (consumer), stats f32, mu f32 [M], aout f16 [M,N] (producer), eps of the folded LayerNorm.
+ * The consumer stages its 256 rows' partial sums in LDS: K <= 3008 (cfg 57) / 3968 (cfg 64) for
+ * per-channel weights, K <= 1728 / 2688 for grouped ones (3-slot rings), else SAMQ_ERR_UNSUPPORTED. */
 int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
                         const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N, int K,
                         int groupsize, int epilogue, int cfg, const float* gamma, const float* gw,
@@ -137,12 +139,21 @@ int samq_w8a8_gemm(const int8_t* A, int64_t lda, const int8_t* wpacked, const fl
 /* W4A8 GEMM: GPTQ int4 weights (QuantLinear buffers, gptq_triton/quant_linear.py:81-85, repacked
  * with samq_w4_repack_layout(..., layout 3, ...)) x int8 activation codes (fq_vit QAct on the
  * QuantLinear input, SURVEY.md §8c "Oracle W4A8"): y = float(sum_k A (q - zp)) * a_scale *
- * wscale[n] + bias[n]; wscale = the QuantLinear scales as f32 [N]; groupsize must be -1 (else
- * SAMQ_ERR_UNSUPPORTED); epilogues BIAS/BIAS_GELU (f16 out), RESADD_F32/F32, Q8/Q8_GELU. */
+ * wscale[n] + bias[n]; wscale = the QuantLinear scales as f32 [G, N] (G = 1 per-channel);
+ * epilogues BIAS/BIAS_GELU (f16 out), RESADD_F32/F32, Q8/Q8_GELU.  groupsize -1 (== K), or a
+ * multiple of 128 (grouped weights, quant_linear.py:324-335: per group g = k / groupsize the
+ * exact int32 sum over the group times wscale[g, n], summed in f32; qzeros [G, N/8]); other
+ * groupsizes SAMQ_ERR_UNSUPPORTED. */
 int samq_w4a8_gemm(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
                    const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N,
                    int K, int groupsize, int epilogue, float a_scale, float out_scale,
                    hipStream_t stream);
+/* The same with an explicit tile config (0 = automatic; per-channel: as samq_i8_gemm_cfg; grouped:
+ * 83 128x128, 84 64x64, 87 128x64, 88 64x128). */
+int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                       const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N,
+                       int K, int groupsize, int epilogue, float a_scale, float out_scale, int cfg,
+                       hipStream_t stream);
 
 /* Both int8 GEMMs with an explicit weight format (0 = W8 packed, 1 = W4 layout 3) and tile
  * config (0 = automatic; 81 256x256, 82 128x256, 83 128x128, 84 64x64); for tuning and tests. */

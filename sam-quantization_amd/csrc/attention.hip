@@ -35,14 +35,6 @@ namespace samq {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
-template <int N, typename F, int I = 0>
-__device__ __forceinline__ void static_for(F&& f) {   // f(integral_constant<int, 0..N-1>)
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, F, I + 1>(static_cast<F&&>(f));
-  }
-}
-
 __device__ __attribute__((aligned(16))) _Float16 g_zero16[8];   // zero source for pad slots
 
 struct AttnParams {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <type_traits>
 
 #include "../../include/samq.h"
 
@@ -84,15 +85,20 @@ __device__ __forceinline__ float2_t gelu_fast2(float2_t x) {
 }
 
 // clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
-// quantizer/uniform.py:31-36), branch-free: q = fl(v * inv) with inv = fl(1/s), then one Markstein
-// correction q' = fl(q + fl(v - s q) inv) (both steps fused multiply-adds; the remainder v - s q is
-// exact) gives fl(v / s) itself -- checked against exact rational division on 1.2e5 operand pairs
-// including +-2 ulp around every .5 tie (tools/check_markstein.py).  Non-finite q (overflow) keeps
-// q, so the clamp sees +-inf as the true division would.
+// quantizer/uniform.py:31-36), branch-free.  q0 = fl(v * inv) with inv = fl(1/s) can be ~1.5 ulp
+// off v/s -- outside Markstein's precondition (a faithful q) -- so one correction is not provably
+// fl(v / s) (it failed on none of ~6e6 adversarial operands, but a quotient within ~2^-22 ulp of a
+// rounding midpoint could flip).  The first correction q1 = fl(q0 + fl(v - s q0) inv) is faithful
+// (error ~0.5 ulp + 2^-23 ulp); the second, q2 = fl(q1 + (v - s q1) inv) with an EXACT remainder,
+// is fl(v / s) by Markstein's theorem (inv within half an ulp of 1/s, round to nearest, no
+// overflow / subnormal quotient in the quantiser's range).  Four FMAs, no division, no branch;
+// tools/check_markstein.py checks both forms against exact rational division.  Non-finite q0
+// (overflow) keeps q0, so the clamp sees +-inf as the true division would.
 __device__ __forceinline__ float q8_exact(float v, float s, float inv) {
   const float q = v * inv;
-  const float qc = __builtin_fmaf(__builtin_fmaf(-q, s, v), inv, q);
-  const float r = __builtin_rintf(__builtin_isfinite(q) ? qc : q);
+  const float q1 = __builtin_fmaf(__builtin_fmaf(-q, s, v), inv, q);
+  const float q2 = __builtin_fmaf(__builtin_fmaf(-q1, s, v), inv, q1);
+  const float r = __builtin_rintf(__builtin_isfinite(q) ? q2 : q);
   return fminf(fmaxf(r, -128.f), 127.f);
 }
 
@@ -137,6 +143,15 @@ __device__ __forceinline__ float wave_max(float v) {
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, k = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {   // f(integral_constant<int, 0..N-1>)
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
 }
 
 }  // namespace samq

@@ -32,6 +32,7 @@ struct I8Epi {
   const int8_t* R;
   int64_t ldr;
   int rmod;               // > 0: residual row = output row % rmod (pos_embed codes shared by images)
+  int kpg;                // grouped W4 (GRP kernels): K tiles (128) per weight group
 };
 
 // Implicit-GEMM A operand (AG != 0): the int8 codes are gathered from an image / feature map
@@ -78,8 +79,10 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
 // is row-contiguous 16-byte vectors.  Shared by the v3-style and the ping-pong int8 kernels.
 // ZPS: the sums exclude the zero point (acc = sum a * q) and the epilogue subtracts zp[n] * S[m]
 // (zpv = this lane's zp per column block, ssum = S of the wave's WM rows; int32-exact)
-template <int TM, int TN, int WN, int EPI, bool ZPS = false>
-__device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], const int (&col)[TN],
+// Grouped W4 (float accumulators, the group scales already applied): wscale == nullptr, the
+// factor is a_scale alone.
+template <int TM, int TN, int WN, int EPI, bool ZPS = false, typename AccV = int16_t_v>
+__device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int (&col)[TN],
                                             const float* __restrict__ wscale, const float* __restrict__ bias,
                                             const I8Epi& ep_args, float* ep, void* __restrict__ Cout, int64_t ldc,
                                             int M, int row_base, int col_base, int lane,
@@ -88,7 +91,7 @@ __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], cons
   float csc[TN], cb[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
-    csc[t] = ep_args.a_scale * wscale[col[t]];
+    csc[t] = wscale ? ep_args.a_scale * wscale[col[t]] : ep_args.a_scale;
     cb[t] = bias ? bias[col[t]] : 0.0f;
   }
   constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
@@ -101,7 +104,7 @@ __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], cons
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
-        int a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
+        auto a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
         if constexpr (ZPS) {
           a0 -= zpv[t] * ssum[i * 32 + rl];
           a1 -= zpv[t] * ssum[i * 32 + rl + 1];
@@ -189,7 +192,14 @@ __device__ __forceinline__ void i8_epilogue(const int16_t_v (&acc)[TM][TN], cons
 }
 
 // ------------------------------------------------------------------ GEMM
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS>
+// GRP (W4 only): grouped GPTQ weights, w = s[g, n] (q - zp[g, n]) with g = k / groupsize and the
+// groupsize a multiple of the 128-deep K tile (ep_args.kpg tiles per group).  The int32 MFMA sums of
+// one group are exact (|sum| <= 128 * 127 * 16 per tile); at each group end they are scaled by the
+// group's f32 scale into f32 accumulators (one fma per element) and restarted; the zero point of
+// the group is applied per byte in the unpack as for per-channel weights.  wscale is the f32
+// [G, N] scale table; the next group's zero / scale words are loaded one K tile ahead, before the
+// tile's LDS-DMA pieces (so the ring's counted vmcnt covers them).
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS, bool GRP = false>
 __global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
                     const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
@@ -210,6 +220,7 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   constexpr int NPW = (NT + NW - 1) / NW;
   constexpr int STAGE = A_BYTES + NB * 1024;
   static_assert(TM >= 1 && TN >= 1 && NPW <= 15, "bad tile");
+  static_assert(!GRP || (BFMT == BF_W4 && AG == AG_ROWS), "grouped: W4 weights, row-major A");
 
   __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
 
@@ -288,12 +299,27 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   }
 
   int16_t_v acc[TM][TN];
+  float16_t facc[GRP ? TM : 1][GRP ? TN : 1];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+      for (int r = 0; r < 16; ++r) {
+        acc[i][j][r] = 0;
+        if constexpr (GRP) facc[i][j][r] = 0.f;
+      }
+  const int kpg = GRP ? ep_args.kpg : 1;
+  float gsc[TN], nsc[TN];   // GRP: the current / next group's scales of this lane's columns
+  uint32_t nzp[TN];
+  if constexpr (GRP) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      gsc[t] = wscale[col[t]];
+      nsc[t] = gsc[t];
+      nzp[t] = zpx[t];
+    }
+  }
 
   int a_off[TM], a_swz[TM];
 #pragma unroll
@@ -313,6 +339,15 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
     if (STAGES > 2) {
       if (kt + 1 < kt_count) vm_wait_i8<NPW>(); else vm_wait_i8<0>();
       __builtin_amdgcn_s_barrier();
+      if (GRP && kt + 1 < kt_count && (kt + 1) % kpg == 0) {   // next group's zero / scale words
+        const int g = (kt + 1) / kpg;
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          const uint32_t zw = qzeros[(int64_t)g * (N / 8) + (col[t] >> 3)];
+          nzp[t] = (((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u) * 0x01010101u;
+          nsc[t] = wscale[(int64_t)g * N + col[t]];
+        }
+      }
       if (kt + 2 < kt_count) {
         int s2 = slot + 2;
         s2 = s2 >= STAGES ? s2 - STAGES : s2;
@@ -321,6 +356,15 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
     } else {
       vm_wait_i8<0>();
       __builtin_amdgcn_s_barrier();            // tile kt landed; everyone is done with tile kt-1
+      if (GRP && kt + 1 < kt_count && (kt + 1) % kpg == 0) {
+        const int g = (kt + 1) / kpg;
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          const uint32_t zw = qzeros[(int64_t)g * (N / 8) + (col[t] >> 3)];
+          nzp[t] = (((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u) * 0x01010101u;
+          nsc[t] = wscale[(int64_t)g * N + col[t]];
+        }
+      }
       if (kt + 1 < kt_count) issue(kt + 1, slot ^ 1);
     }
     const char* abase = smem + slot * STAGE;
@@ -355,6 +399,22 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
         for (int i = 0; i < TM; ++i) acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf, acc[i][t], 0, 0, 0);
       }
     }
+    if (GRP && ((kt + 1) % kpg == 0 || kt + 1 == kt_count)) {   // group end: scale the exact sums in
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            facc[i][t][r] = __builtin_fmaf((float)acc[i][t][r], gsc[t], facc[i][t][r]);
+            acc[i][t][r] = 0;
+          }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        zpx[t] = nzp[t];
+        gsc[t] = nsc[t];
+      }
+    }
     if (STAGES > 2) slot = slot + 1 == STAGES ? 0 : slot + 1;
     else slot ^= 1;
   }
@@ -362,8 +422,12 @@ void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __res
   // ---- epilogue (LDS-staged per 32-row slice; see gemm_w4a16.hip v3)
   static_assert(NW * 32 * WN * 4 <= STAGES * STAGE, "epilogue staging does not fit the LDS ring");
   __syncthreads();
-  i8_epilogue<TM, TN, WN, EPI>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * 32 * WN * 4), Cout, ldc, M,
-                               m0 + wm * WM, n0 + wn * WN, lane);
+  if constexpr (GRP)
+    i8_epilogue<TM, TN, WN, EPI, false, float16_t>(facc, col, nullptr, bias, ep_args, (float*)(smem + wave * 32 * WN * 4),
+                                                   Cout, ldc, M, m0 + wm * WM, n0 + wn * WN, lane);
+  else
+    i8_epilogue<TM, TN, WN, EPI>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * 32 * WN * 4), Cout, ldc, M,
+                                 m0 + wm * WM, n0 + wn * WN, lane);
 }
 
 // ------------------------------------------------------------------ W4A8 ping-pong GEMM
@@ -395,6 +459,9 @@ __device__ __forceinline__ void i8_vm_wait_le(int n) {   // s_waitcnt vmcnt(n) f
 // S[m] = sum_k a[m, k] accumulated from the staged A tile by v_dot4 against ones (wave wn sums the
 // 32 rows of its M block wn, 8 dot4 + 2 LDS reads per phase; the 4 waves of an M half share the
 // sums through LDS at the end).  Integer-exact: identical outputs.
+// VAR & 16: the phase's LDS-DMA pieces spread through the MFMA burst (one after every 16 / np
+// MFMAs) instead of issued after it, where they queue in the TA behind the other MFMA-half waves'
+// pieces while the MFMA pipe drains and the partner group waits at the barrier.
 // VAR (tuning build only, timing experiments that compute wrong results): 1 no zero-point
 // subtraction in the unpack, 2 no MFMA, 4 no restaging
 template <int EPI, int STAGES, int LA, int VAR = 0>
@@ -508,13 +575,14 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   __builtin_amdgcn_sched_barrier(0);
 
   int slot = 0;
+  constexpr bool SPREAD = (VAR & 16) != 0;
   for (int kt = 0; kt < kt_count; ++kt) {
     const char* st = smem + slot * STAGE;
     const int ahead = kt + LA;
     const bool pf = ahead < kt_count && !(VAR & 4);
     const int sa = slot + LA >= STAGES ? slot + LA - STAGES : slot + LA;   // (kt + LA) % STAGES
-#pragma unroll
-    for (int p = 0; p < NPH; ++p) {
+    static_for<NPH>([&](auto pc_) {
+      constexpr int p = decltype(pc_)::value;
       // ---------------- load half
       if (p == NPH - 1 && kt + 1 < kt_count) {
         // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far
@@ -565,21 +633,39 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
       __builtin_amdgcn_sched_barrier(0);
       // ---------------- MFMA half
       __builtin_amdgcn_s_setprio(1);
+      if constexpr (SPREAD) {
+        static_assert(!(VAR & 2), "spread: product MFMA halves only");
+        constexpr int P0 = i8_pre(p, NPW, NPH), NP = i8_pre(p + 1, NPW, NPH) - P0, NMF = 2 * TM * TN;
+        static_for<NMF>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          constexpr int s = q / (TM * TN), i = (q / TN) % TM, t = q % TN;
+          acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+          static_for<NPW>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (k < NP && q + 1 == ((2 * k + 1) * NMF) / (2 * NP)) {
+              __builtin_amdgcn_sched_barrier(0);
+              if (pf) issue(ahead, sa, P0 + k, P0 + k + 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          });
+        });
+      } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int t = 0; t < TN; ++t) {
-            if (VAR & 2) acc[i][t][0] += af[i][s][0] ^ bf[t][s][1];
-            else acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
-          }
-      if (pf) issue(ahead, sa, i8_pre(p, NPW, NPH), i8_pre(p + 1, NPW, NPH));
+            for (int t = 0; t < TN; ++t) {
+              if (VAR & 2) acc[i][t][0] += af[i][s][0] ^ bf[t][s][1];
+              else acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+            }
+        if (pf) issue(ahead, sa, i8_pre(p, NPW, NPH), i8_pre(p + 1, NPW, NPH));
+      }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-    }
+    });
     slot = slot == STAGES - 1 ? 0 : slot + 1;
   }
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
@@ -606,10 +692,10 @@ struct I8Args {
   const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep; I8Gather ga;
 };
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST, int AG = AG_ROWS>
+template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST, int AG = AG_ROWS, bool GRP = false>
 static int launch_i8(const I8Args& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
-  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST, AG>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST, AG, GRP>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
                      a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep, a.ga);
   SAMQ_LAUNCH_CHECK("i8_gemm launch");
   return SAMQ_OK;
@@ -636,6 +722,9 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 86:
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 86 is the W4 ping-pong kernel");
+    case 93:   // cfg 86 with the LDS-DMA pieces spread through the MFMA bursts
+      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
+      else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 93 is the W4 ping-pong kernel");
 #ifdef SAMQ_TUNING
     case 95: case 96: case 97:   // timing-only (wrong results): no zero point / no MFMA / no restaging
       if constexpr (BF == BF_W4) {
@@ -662,7 +751,7 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
+  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
     case 92: return 32; default: return 0; }
 }
 
@@ -691,6 +780,31 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
   if (N % 256 == 0 && t256 >= 512) return 82;
   if (N % 128 == 0 && M >= 256) return 83;
   return 84;
+}
+
+// grouped W4 (ep.kpg K tiles per group): the v3-style kernel with f32 group accumulators beside the
+// int32 ones -- wave tiles of at most 64x64 (the pair of accumulator sets must fit the registers)
+template <int EPI>
+static int launch_i8_grouped(const I8Args& a, int cfg, hipStream_t st) {
+  switch (cfg) {
+    case 83: return launch_i8<128, 128, 2, 2, EPI, BF_W4, 3, AG_ROWS, true>(a, st);
+    case 84: return launch_i8<64, 64, 2, 2, EPI, BF_W4, 3, AG_ROWS, true>(a, st);
+    case 87: return launch_i8<128, 64, 2, 2, EPI, BF_W4, 3, AG_ROWS, true>(a, st);
+    case 88: return launch_i8<64, 128, 2, 2, EPI, BF_W4, 3, AG_ROWS, true>(a, st);
+    default: return fail(SAMQ_ERR_INVALID, "w4a8_gemm: grouped weights take tile configs 83 / 84 / 87 / 88");
+  }
+}
+
+static int i8_dispatch_grouped(const I8Args& a, int epi, int cfg, hipStream_t st) {
+  switch (epi) {
+    case SAMQ_EPI_BIAS: return launch_i8_grouped<SAMQ_EPI_BIAS>(a, cfg, st);
+    case SAMQ_EPI_BIAS_GELU: return launch_i8_grouped<SAMQ_EPI_BIAS_GELU>(a, cfg, st);
+    case SAMQ_EPI_RESADD_F32: return launch_i8_grouped<SAMQ_EPI_RESADD_F32>(a, cfg, st);
+    case SAMQ_EPI_F32: return launch_i8_grouped<SAMQ_EPI_F32>(a, cfg, st);
+    case SAMQ_EPI_Q8: return launch_i8_grouped<SAMQ_EPI_Q8>(a, cfg, st);
+    case SAMQ_EPI_Q8_GELU: return launch_i8_grouped<SAMQ_EPI_Q8_GELU>(a, cfg, st);
+    default: return fail(SAMQ_ERR_INVALID, "w4a8_gemm: unknown epilogue for grouped weights");
+  }
 }
 
 static int i8_dispatch(const I8Args& a, int bfmt, int epi, int cfg, hipStream_t st) {
@@ -795,12 +909,38 @@ extern "C" int samq_w8a8_gemm(const int8_t* A, int64_t lda, const int8_t* wpacke
                           mid_scale, res_scale, out_scale, 0, stream);
 }
 
+extern "C" int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                                  const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N,
+                                  int K, int groupsize, int epilogue, float a_scale, float out_scale, int cfg,
+                                  hipStream_t stream) {
+  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES, SAMQ_ERR_INVALID, "w4a8_gemm: Q8_RES is a W8A8 epilogue");
+  if (groupsize == -1 || groupsize == K)
+    return samq_i8_gemm_cfg(A, lda, BF_W4, wpacked, wscale, qzeros, bias, C, ldc, nullptr, 0, M, N, K, epilogue,
+                            a_scale, 0.f, 0.f, out_scale, cfg, stream);
+  // grouped weights (gptq_triton/quant_linear.py:324-335: per-group scale / zero rows)
+  SAMQ_REQUIRE(A && wpacked && wscale && qzeros && C, SAMQ_ERR_INVALID, "w4a8_gemm: null pointer");
+  SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 128 == 0 && N % 64 == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm: K % 128 == 0 and N % 64 == 0 required");
+  SAMQ_REQUIRE(groupsize > 0 && groupsize % 128 == 0, SAMQ_ERR_UNSUPPORTED,
+               "w4a8_gemm: grouped weights need a groupsize that is a multiple of 128 (the int8 K tile)");
+  SAMQ_REQUIRE(lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm: A must be 16-byte aligned with lda >= K, lda % 16 == 0");
+  const bool q8 = epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_GELU;
+  const bool f32 = epilogue == SAMQ_EPI_RESADD_F32 || epilogue == SAMQ_EPI_F32;
+  SAMQ_REQUIRE(ldc >= N && ((uintptr_t)C & 15) == 0 && ldc % (q8 ? 16 : (f32 ? 4 : 8)) == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm: C must be 16-byte aligned rows, ldc >= N");
+  SAMQ_REQUIRE(!q8 || out_scale > 0.f, SAMQ_ERR_INVALID, "w4a8_gemm: quantising epilogue needs out_scale > 0");
+  if (M == 0) return SAMQ_OK;
+  if (cfg <= 0) cfg = N % 128 == 0 && M >= 1024 ? 83 : 84;
+  SAMQ_REQUIRE(i8_cfg_bn(cfg) > 0 && N % i8_cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a8_gemm: N not divisible by tile");
+  I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
+           I8Epi{a_scale, 0.f, 0.f, out_scale, nullptr, 0, 0, groupsize / 128}, I8Gather{0, 0, 0}};
+  return i8_dispatch_grouped(a, epilogue, cfg, stream);
+}
+
 extern "C" int samq_w4a8_gemm(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
                               const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N, int K,
                               int groupsize, int epilogue, float a_scale, float out_scale, hipStream_t stream) {
-  SAMQ_REQUIRE(groupsize == -1 || groupsize == K, SAMQ_ERR_UNSUPPORTED,
-               "w4a8_gemm: only per-channel weights (groupsize -1) are supported with int8 activations");
-  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES, SAMQ_ERR_INVALID, "w4a8_gemm: Q8_RES is a W8A8 epilogue");
-  return samq_i8_gemm_cfg(A, lda, BF_W4, wpacked, wscale, qzeros, bias, C, ldc, nullptr, 0, M, N, K, epilogue,
-                          a_scale, 0.f, 0.f, out_scale, 0, stream);
+  return samq_w4a8_gemm_cfg(A, lda, wpacked, wscale, qzeros, bias, C, ldc, M, N, K, groupsize, epilogue, a_scale,
+                            out_scale, 0, stream);
 }

@@ -1149,6 +1149,22 @@ __device__ __forceinline__ void xcd_tile(int bid, int tiles_m, int tiles_n, bool
   nt = t % tiles_n;
 }
 
+// LDS budget of a ping-pong config (the kernel static_asserts its own SMEM against it).  The
+// LayerNorm-fold consumer stages its workgroup's row partial sums (BM rows x K/64 float2) behind
+// the epilogue slices and the (delta, rstd) table, in the LDS the ring leaves free once the main
+// loop is done: LNF_KMAX is the largest consumer K that fits (samq_w4a16_gemm_lnf checks it).
+template <int WAVES_M, int TM, int TN, int STAGES, int EPI, int VAR>
+struct Pp2Lds {
+  static constexpr int NW = 8, WM = TM * 32, WN = TN * 32, BM = WAVES_M * WM, BN = (NW / WAVES_M) * WN;
+  static constexpr bool GR = (VAR & 512) != 0, M16 = (VAR & 16) != 0;
+  static constexpr int GRB = GR ? (BN * 2 / 16 + BN / 32) * 16 : 0;
+  static constexpr int STAGE = BM * 128 + (BN / 32) * 1024 + GRB;
+  static constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : (WN > 64 ? 16 : 32) * WN * 4;
+  static constexpr int RI_BYTES = (EPI == SAMQ_EPI_BIAS_LNF || EPI == SAMQ_EPI_GELU_LNF) ? BM * 8 : 0;
+  static constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES + RI_BYTES ? STAGES * STAGE : NW * EP_BYTES + RI_BYTES;
+  static constexpr int LNF_KMAX = ((SMEM - NW * EP_BYTES - RI_BYTES) / (BM * 8)) * 64;
+};
+
 __host__ __device__ constexpr int pp2_pre(int p, int npw, int nph, int first) {   // pieces before phase p
   return p <= first ? 0 : (npw * (p - first)) / (nph - first);
 }
@@ -1210,12 +1226,16 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
   constexpr bool M16 = (VAR & 16) != 0;
   constexpr bool TE = (VAR & 128) != 0;   // transposed accumulators + direct epilogue (te_store4)
+  // VAR & 16384: LDS-DMA pieces spread through the MFMA burst (see the MFMA half)
+  constexpr bool DMA_SPREAD = (VAR & 16384) != 0;
+  static_assert(!DMA_SPREAD || !(DMA_LOAD || TE || (VAR & 2)), "DMA spread: product MFMA halves only");
   constexpr int KS32 = 2 / NPH;                  // M16: k32 steps per phase
   constexpr int EP_ROWS = WN > 64 ? 16 : 32;
   constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : EP_ROWS * WN * 4;
   // LN-fold consumers: per-wave (delta, rstd) of its WM rows behind the epilogue slices
   constexpr int RI_BYTES = lnf_consumer(EPI) ? BM * 8 : 0;
   constexpr int SMEM = STAGES * STAGE > NW * EP_BYTES + RI_BYTES ? STAGES * STAGE : NW * EP_BYTES + RI_BYTES;
+  static_assert(SMEM == Pp2Lds<WAVES_M, TM, TN, STAGES, EPI, VAR>::SMEM, "Pp2Lds mirrors this layout");
   static_assert(!M16 || NPH <= 2, "M16: one or two phases per K tile");
   static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
   static_assert(LA >= 2 && LA < STAGES, "ring");
@@ -1403,8 +1423,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     const int sa = slot + LA >= STAGES ? slot + LA - STAGES : slot + LA;   // (kt + LA) % STAGES
     u32x4 bw[TN];
     uint32_t bw16[TN][2][2];
-#pragma unroll
-    for (int p = 0; p < NPH; ++p) {
+    static_for<NPH>([&](auto pc_) {   // phases: p a constant (folds the DMA piece schedule)
+      constexpr int p = decltype(pc_)::value;
       // ---------------- load half
       if (p == NPH - 1 && kt + 1 < kt_count) {
         // K tile kt+1 retired: newer = whole tiles kt+2 .. kt+LA-1 + this tile's pieces so far.
@@ -1487,7 +1507,32 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       if (VAR & 4) stamp(1);
       // ---------------- MFMA half
       if (!(VAR & 256)) __builtin_amdgcn_s_setprio(1);
-      if constexpr (M16) {
+      if constexpr (DMA_SPREAD) {
+        // the phase's LDS-DMA pieces spread through the MFMA burst (one after every NMF / np
+        // MFMAs) instead of after it: issued after the last MFMA they queue behind the other
+        // MFMA-half waves' pieces in the TA while the MFMA pipe drains, and the partner group
+        // waits at the barrier for that tail (pp2 stamps: MFMA half ~690 cycles for 512)
+        constexpr int P0 = pp2_pre(p, NPW, NPH, 0), NP = pp2_pre(p + 1, NPW, NPH, 0) - P0;
+        constexpr int NMF = M16 ? KS32 * 2 * TM * TN * 2 : KPP * TM * TN;
+        static_for<NMF>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          if constexpr (M16) {
+            constexpr int s = q / (2 * TM * TN * 2), i = (q / (TN * 2)) % (2 * TM), t = (q / 2) % TN, h = q % 2;
+            acc16[i][t][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af16[i][s], bf16[t][h][s], acc16[i][t][h], 0, 0, 0);
+          } else {
+            constexpr int s = q / (TM * TN), i = (q / TN) % TM, t = q % TN;
+            acc[i][t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i][s], bf[t][s], acc[i][t], 0, 0, 0);
+          }
+          static_for<NPW>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if constexpr (k < NP && q + 1 == ((2 * k + 1) * NMF) / (2 * NP)) {
+              __builtin_amdgcn_sched_barrier(0);
+              if (pf) issue(ahead, sa, P0 + k, P0 + k + 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          });
+        });
+      } else if constexpr (M16) {
 #pragma unroll
         for (int s = 0; s < KS32; ++s)
 #pragma unroll
@@ -1515,7 +1560,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       }
       // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
       // the barrier otherwise; WAR-safe in every phase: see header)
-      if (pf && !DMA_LOAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
+      if (pf && !DMA_LOAD && !DMA_SPREAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
       // GR: tile kt+1 starts a group -> its row into registers (every wave's retire wait for tile
       // kt+1, wave 0's included, precedes the barrier that opened this MFMA half)
       if (GR && !G_NOROW && p == NPH - 1 && kt + 1 < kt_count && gk + 1 == kpg)
@@ -1526,7 +1571,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (VAR & 4) stamp(3);
-    }
+    });
     slot = slot == STAGES - 1 ? 0 : slot + 1;
     if (GR) gk = gk + 1 == kpg ? 0 : gk + 1;
   }
@@ -1537,6 +1582,22 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
     atomicAdd(&g_pp_stamps[4], (unsigned long long)kt_count * NPH);
   }
 
+  if constexpr ((VAR & 32768) != 0) {   // timing-only (tuning build): no epilogue -- keeps the sums alive
+    float z = 0.f;
+    if constexpr (M16) {
+#pragma unroll
+      for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) z += acc16[i][t][0][0] + acc16[i][t][1][3];
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < TN; ++t) z += acc[i][t][0] + acc[i][t][15];
+    }
+    if (z == 1234.5f) ((float*)Cout)[tid] = z;
+    return;
+  }
   if constexpr (M16 && TE) {
     // lane (ql, g16) holds row 16 i + ql, columns 32 t + 16 h + 4 g16 .. +3 of the wave's tile
 #pragma unroll
@@ -1646,6 +1707,12 @@ static int launch_v4(const GemmArgs& a, hipStream_t st) {
 template <int WMW, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
 static int launch_pp2(const GemmArgs& a, hipStream_t st) {
   constexpr int BM = WMW * TM * 32, BN = (8 / WMW) * TN * 32;
+  if (EPI == SAMQ_EPI_BIAS_LNF || EPI == SAMQ_EPI_GELU_LNF) {
+    // the consumer's row partials must fit the LDS the ring frees (a grouped cfg 57
+    // ring leaves room for K <= 1728 only)
+    constexpr int kmax = Pp2Lds<WMW, TM, TN, STAGES, EPI, VAR>::LNF_KMAX;
+    if (a.K > kmax) return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm_lnf: consumer K exceeds this config's LDS row-partial budget");
+  }
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
   hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
                      a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64, a.lnf);
@@ -1675,7 +1742,7 @@ static int launch_silu(const GemmArgs& a, hipStream_t st) {
 
 template <int EPI, bool GR>
 static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
-  if (cfg >= 50 && cfg < 100) {   // ping-pong kernels
+  if (cfg >= 50 && cfg < 200) {   // ping-pong kernels
     if (GR) {   // grouped weights: the per-group scale / zero row rides in the ring (VAR & 512)
       switch (cfg) {
         // 3 slots, lookahead 2: four 40 KiB stages fill the 160 KiB LDS, the group row needs 640 B more
@@ -1694,6 +1761,9 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 62: return launch_pp2<4, 2, 4, 2, 4, 3, EPI>(a, st);   // 4x2 waves (64x128 each): A read 2x, B 4x
       case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);  // cfg 57 on 16x16x32 MFMA
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
+      // cfg 57 / 64 with the LDS-DMA pieces spread through the MFMA burst (VAR & 16384)
+      case 100: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 16384>(a, st);
+      case 101: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 16384>(a, st);
 #ifdef SAMQ_TUNING
       // tuning build only (make tuning): untested shapes and TIMING-ONLY variants that compute
       // wrong results on purpose -- never reachable through the product library
@@ -1737,6 +1807,9 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // pieces per 256x256-equivalent of work); N % 512 == 0 (lin1)
       case 97: return launch_pp2<1, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
       case 98: return launch_pp2<1, 4, 2, 2, 5, 4, EPI, 4096>(a, st);
+      // timing-only: cfg 57 / 64 without the epilogue (the per-tile epilogue cost)
+      case 102: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 32768>(a, st);
+      case 103: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 32768>(a, st);
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
       case 73: {   // timing experiment: cfg 57 with per-segment s_memtime stamps (synchronous)
@@ -1832,6 +1905,7 @@ static int cfg_bn(int cfg) {
                  case 74: case 75: case 76: case 77: case 78: case 79: return 256;
                  case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
                  case 97: case 98: return 512;
+                 case 100: case 101: case 102: case 103: return 256;
                  default: return 0; }
 }
 
@@ -1946,8 +2020,8 @@ extern "C" int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wp
   } else if (epilogue == SAMQ_EPI_BIAS_LNF || epilogue == SAMQ_EPI_GELU_LNF) {
     SAMQ_REQUIRE(gw && bw, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: the consumer needs gw and bw");
     // the workgroup's row partial sums (256 rows x K/64 pairs) are staged in the LDS the ring
-    // leaves free in the epilogue (>= 94 KiB on both ping-pong forms)
-    SAMQ_REQUIRE(K <= 2048, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: consumer K must be <= 2048");
+    // leaves free in the epilogue: Pp2Lds::LNF_KMAX per config (launch_pp2 checks it -- K <= 3008
+    // for cfg 57, 3968 for cfg 64 per-channel; 1728 / 2688 for grouped weights' 3-slot rings)
   } else {
     return fail(SAMQ_ERR_INVALID, "w4a16_gemm_lnf: epilogue must be RESADD_LNF, BIAS_LNF or GELU_LNF");
   }

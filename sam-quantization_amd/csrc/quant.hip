@@ -11,7 +11,7 @@ namespace samq {
 template <bool IN_F16, bool OUT_FQ>
 __global__ __launch_bounds__(256) void quantize_kernel(const void* __restrict__ x, void* __restrict__ y, int64_t n,
                                                        float s) {
-  const float inv = 1.0f / s;   // q8_exact (common.h): multiply + one Markstein correction
+  const float inv = 1.0f / s;   // q8_exact (common.h): multiply + two Markstein corrections
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4 + (n & 3); i += stride) {

@@ -67,6 +67,8 @@ SIGNATURES = {
                               _f32, _f32, _f32, _f32, _vp]),
     "samq_w4a8_gemm": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
                               _f32, _f32, _vp]),
+    "samq_w4a8_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
+                                  _f32, _f32, _i32, _vp]),
     "samq_i8_gemm_cfg": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
                                 _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "samq_w8a8_conv_gemm": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,

@@ -191,17 +191,26 @@ class EncoderEngine:
             return
         ops.patch_embed(img.to(torch.float32).contiguous(), self.pe_w32, self.pe_b, pos, p, out=x32)
 
-    def block_w4a8(self, p: _BlockPlan, bufs) -> None:
+    def block_w4a8(self, p: _BlockPlan, bufs, mark=None) -> None:
         """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded
-        into LN / the GELU epilogue / the attention's store), int8 MFMA GEMMs."""
+        into LN / the GELU epilogue / the attention's store), int8 MFMA GEMMs.  ``mark(k)`` as in
+        ``block``."""
+        mark = mark or (lambda k: None)
         x, xn8, qkv, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att8"], bufs["hid8"]
         ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
+        mark(0)
         p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
+        mark(1)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8, out_scale=p.s_proj)
+        mark(2)
         p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
+        mark(3)
         ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
+        mark(4)
         p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
+        mark(5)
         p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
+        mark(6)
 
     # ---------------------------------------------------------------- LayerNorm fold
     def _fold_usable(self, rows: int) -> bool:
@@ -222,32 +231,43 @@ class EncoderEngine:
             p.lin1_gw, p.lin1_bw = p.lin1.ln_fold_constants(p.ln2_w, p.ln2_b)
         self._fold_ready = True
 
-    def block_fold(self, i: int, bufs) -> None:
+    def block_fold(self, i: int, bufs, mark=None) -> None:
         """W4A16 block with the LayerNorms folded into the GEMMs (samq_w4a16_gemm_lnf, include/samq.h):
         proj's residual epilogue emits f16((x - mu) * gamma2) + per-row partial sums, lin1's
         epilogue applies LN2 algebraically (rstd * (acc - delta * gamma2.W1) + beta2.W1 + b1, GELU);
         lin2's residual epilogue does the same for the next block's norm1 and its qkv consumes it.
-        Block 0's norm1 stays a LayerNorm kernel (it also writes the row means mu)."""
+        Block 0's norm1 stays a LayerNorm kernel (it also writes the row means mu).  ``mark(k)``
+        runs at the place of ``block``'s launch k (a folded LayerNorm's mark right after the
+        launch that absorbed it), so the lane stagger gates at the same point as unfolded."""
+        mark = mark or (lambda k: None)
         p = self.plans[i]
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
         st, mu = bufs["stats"], bufs["mu"]
         if i == 0:
             ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw, mean_out=mu)
+            mark(0)
             p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
         else:
+            mark(0)   # norm1 was folded into the previous block's lin2
             p.qkv.forward_lnf(xn, ops.EPI_BIAS_LNF, qkv, st, mu, gw=p.qkv_gw, bw=p.qkv_bw, eps=p.ln1_eps)
+        mark(1)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        mark(2)
         p.proj.forward_lnf(att, ops.EPI_RESADD_LNF, x, st, mu, gamma=p.ln2_w, aout=xn)
+        mark(3)
+        mark(4)   # norm2 folded into proj (producer) / lin1 (consumer)
         p.lin1.forward_lnf(xn, ops.EPI_GELU_LNF, hid, st, mu, gw=p.lin1_gw, bw=p.lin1_bw, eps=p.ln2_eps)
+        mark(5)
         if i + 1 < len(self.plans):
             p.lin2.forward_lnf(hid, ops.EPI_RESADD_LNF, x, st, mu, gamma=self.plans[i + 1].ln1_w, aout=xn)
         else:
             p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
+        mark(6)
 
     def block(self, p: _BlockPlan, bufs, mark=None) -> None:
         """One W4A16 block (7 launches).  ``mark(k)`` (lane stagger) runs after launch k."""
         if self.w4a8:
-            return self.block_w4a8(p, bufs)
+            return self.block_w4a8(p, bufs, mark)
         mark = mark or (lambda k: None)
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
         ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw)
@@ -334,22 +354,18 @@ class EncoderEngine:
 
     def _forward(self, img: torch.Tensor, bufs, out_dtype, gate_event=None) -> torch.Tensor:
         self.embed(img, bufs["x"])
-        if self._fold_ready and self._fold_usable(bufs["x"].numel() // self.C):
-            for i in range(len(self.plans)):
-                self.block_fold(i, bufs)
-            if gate_event is not None:
-                gate_event.record()
-        else:
-            for i, p in enumerate(self.plans):
-                mark = None
-                if gate_event is not None and i == self.lane_stagger // 7:
-                    k0 = self.lane_stagger % 7
-                    mark = lambda k, k0=k0: gate_event.record() if k == k0 else None  # noqa: E731
+        fold = self._fold_ready and self._fold_usable(bufs["x"].numel() // self.C)
+        for i, p in enumerate(self.plans):
+            mark = None
+            if gate_event is not None and i == self.lane_stagger // 7:
+                k0 = self.lane_stagger % 7
+                mark = lambda k, k0=k0: gate_event.record() if k == k0 else None  # noqa: E731
+            if fold:
+                self.block_fold(i, bufs, mark)
+            else:
                 self.block(p, bufs, mark)
-                if mark is not None and self.w4a8:   # the W4A8 block takes no marks: gate after it
-                    gate_event.record()
-            if gate_event is not None and self.lane_stagger // 7 >= len(self.plans):
-                gate_event.record()
+        if gate_event is not None and self.lane_stagger // 7 >= len(self.plans):
+            gate_event.record()
         return self.neck(bufs["x"], out_dtype)
 
     __call__ = forward

@@ -23,7 +23,7 @@ EPI_BIAS_LNF = _lib.EPI_BIAS_LNF
 EPI_GELU_LNF = _lib.EPI_GELU_LNF
 
 # W4A16 tile configs of the product library (include/samq.h, samq_w4a16_gemm_cfg); 0 = automatic
-W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65))
+W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65, 100, 101))
 _Q8_EPIS = (EPI_Q8, EPI_Q8_GELU, EPI_Q8_RES)
 
 
@@ -105,6 +105,9 @@ def w4a16_gated_mlp(a: torch.Tensor, wpacked2: torch.Tensor, scales2: torch.Tens
     ``w4_interleave32`` operands of the two projections."""
     _need_cuda(a, wpacked2, scales2, qzeros2)
     assert a.dtype == torch.float16 and a.stride(-1) == 1
+    # the kernel's 256-column tiles over the interleaved 2N columns (ADVICE r3); the reference's
+    # triton_llama_mlp_4 asserts N % 256 already (gptq_triton/fused_mlp.py:437)
+    assert n % 128 == 0, "w4a16_gated_mlp: N must be a multiple of 128"
     k = a.shape[-1]
     x = a.reshape(-1, k)
     m = x.shape[0]
@@ -427,10 +430,26 @@ def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: to
 
 def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_scale=1.0, out_scale=0.0,
               out=None, groupsize=-1, cfg=0):
-    """GPTQ int4 weights (repacked layout 3) x int8 activation codes (cfg 0 = library pick)."""
-    if groupsize not in (-1, a.shape[-1]):
-        raise NotImplementedError("w4a8_gemm: only groupsize -1 (per-channel) is supported with int8 activations")
-    return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out, cfg=cfg)
+    """GPTQ int4 weights (repacked layout 3) x int8 activation codes (cfg 0 = library pick).
+    ``groupsize`` -1 (per-channel, ``wscale`` f32 [N]) or a multiple of 128 (grouped:
+    ``wscale`` f32 [G, N], ``qzeros`` [G, N/8]; samq_w4a8_gemm_cfg)."""
+    if groupsize in (-1, a.shape[-1]):
+        return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out,
+                       cfg=cfg)
+    if groupsize <= 0 or groupsize % 128:
+        raise NotImplementedError("w4a8_gemm: grouped weights need groupsize % 128 == 0 (the int8 K tile)")
+    _need_cuda(a, wpacked3, wscale, bias, qzeros)
+    assert a.dtype == torch.int8 and wscale.dtype == torch.float32
+    assert bias is None or bias.dtype == torch.float32
+    k = a.shape[-1]
+    assert wscale.numel() == ((k + groupsize - 1) // groupsize) * n, "w4a8_gemm: wscale must be f32 [G, N]"
+    a2 = a.reshape(-1, k)
+    out, o2 = _i8_out(a2, n, epilogue, out, tuple(a.shape[:-1]))
+    status = _lib.load().samq_w4a8_gemm_cfg(
+        _ptr(a2), a2.stride(0), _ptr(wpacked3), _ptr(wscale), _ptr(qzeros), _ptr(bias), _ptr(o2), o2.stride(0),
+        a2.shape[0], n, k, groupsize, epilogue, float(a_scale), float(out_scale), cfg, _stream())
+    _lib.check(status, "w4a8_gemm")
+    return out
 
 
 def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,

@@ -89,9 +89,10 @@ class QuantLinear(nn.Module):
 
     def prepare_w4a8(self) -> dict:
         """Kernel-side buffers of the W4A8 GEMM: int4 weights in the int8-MFMA fragment order
-        (repack layout 3), f32 per-channel scales and bias."""
-        if self.groupsize != self.infeatures:
-            raise NotImplementedError("W4A8 needs per-channel weights (groupsize -1)")
+        (repack layout 3), f32 scales ([G, N]; G = 1 per-channel) and bias.  Grouped weights need
+        a groupsize that is a multiple of 128 (the int8 kernel's K tile)."""
+        if self.groupsize != self.infeatures and self.groupsize % 128:
+            raise NotImplementedError("W4A8 with grouped weights needs groupsize % 128 == 0")
         key = (self.qweight.data_ptr(), self.qweight.device, self.qweight._version, self.scales._version)
         if self._w4a8 is None or self._w4a8["key"] != key:
             self._w4a8 = dict(key=key, packed=ops.w4_repack(self.qweight, layout=3),
@@ -113,8 +114,9 @@ class QuantLinear(nn.Module):
                      out_scale: float = 0.0) -> torch.Tensor:
         """int8 input codes (scale ``a_scale``) x int4 weights on the int8 MFMA."""
         w = self.prepare_w4a8()
+        gs = -1 if self.groupsize == self.infeatures else self.groupsize
         return ops.w4a8_gemm(codes, w["packed"], w["scale"], self.qzeros, self.outfeatures, w["bias"], epilogue,
-                             a_scale, out_scale, out=out, cfg=getattr(self, "i8_cfg", 0))
+                             a_scale, out_scale, out=out, groupsize=gs, cfg=getattr(self, "i8_cfg", 0))
 
     def forward_lnf(self, x: torch.Tensor, epilogue: int, out: torch.Tensor, stats: torch.Tensor, mu: torch.Tensor,
                     **kw) -> torch.Tensor:

@@ -98,7 +98,7 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
         _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
 
 
-@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65])
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
@@ -411,8 +411,9 @@ def test_conv_ops_reject_bad_shapes(cuda):
 
 # ----------------------------------------------------------------------------- LayerNorm fold
 @pytest.mark.parametrize("groupsize", [-1, 128])
-@pytest.mark.parametrize("m,cfg_p,cfg_c", [(8192, 0, 0), (333, 64, 57), (300, 57, 64)])
-def test_w4a16_gemm_lnf_chain(cuda, groupsize, m, cfg_p, cfg_c):
+@pytest.mark.parametrize("m,cfg_p,cfg_c,c", [(8192, 0, 0, 1280), (333, 64, 57, 1280), (300, 57, 64, 1280),
+                                             (300, 57, 64, 2048)])
+def test_w4a16_gemm_lnf_chain(cuda, groupsize, m, cfg_p, cfg_c, c):
     """LayerNorm folded into the GEMMs around it (samq_w4a16_gemm_lnf): the residual producer
     (x += att.Wp + bp; a = f16((x - mu_p) gamma); per-row partial sums) followed by the consumer
     (GELU(LN(x).W1 + b1) from a, the sums and gamma.W1 / beta.W1) against the plain fp32 chain
@@ -420,8 +421,8 @@ def test_w4a16_gemm_lnf_chain(cuda, groupsize, m, cfg_p, cfg_c):
     LayerNorm's mean, here a perturbed copy of the true row mean (what the engine carries)."""
     import samq
     from samq import ops
-    c, n1 = 1280, 2560
-    rng = np.random.Generator(np.random.PCG64(5 + m + groupsize))
+    n1 = 2560
+    rng = np.random.Generator(np.random.PCG64(5 + m + groupsize + c))
     qwp, qzp, scp, bp = _packed_layer(c, c, groupsize, seed=3 + m)
     qw1, qz1, sc1, b1 = _packed_layer(c, n1, groupsize, seed=4 + m)
     att = (rng.standard_normal((m, c), dtype=np.float32)).astype(np.float16)
@@ -483,3 +484,32 @@ def test_w4a16_gemm_lnf_rejects_non_pingpong(cuda):
         lin.forward_lnf(torch.zeros((64, 256), dtype=torch.float16, device=cuda), ops.EPI_RESADD_LNF,
                         torch.zeros((64, 256), device=cuda), st, mu, gamma=torch.ones(256, device=cuda),
                         aout=torch.zeros((64, 256), dtype=torch.float16, device=cuda))
+
+
+@pytest.mark.parametrize("groupsize,cfg,k,ok", [(64, 57, 1728, True), (64, 57, 1792, False), (64, 64, 2688, True),
+                                                 (64, 64, 2752, False), (-1, 57, 3008, True), (-1, 57, 3072, False)])
+def test_w4a16_gemm_lnf_consumer_k_limit(cuda, groupsize, cfg, k, ok):
+    """ADVICE r3: the consumer stages 256 rows x K/64 partial-sum pairs in the LDS its ring frees;
+    a K past the config's budget (grouped cfg 57: 1728) is SAMQ_ERR_UNSUPPORTED instead of a
+    silent LDS overrun.  At the limit itself the launch runs (finite output)."""
+    import samq
+    from samq import ops
+    m, n = 256, 256
+    lin = samq.QuantLinear(4, groupsize, k, n, True).to(cuda)
+    qw, qz, sc, b = _packed_layer(k, n, groupsize, seed=k + cfg)
+    lin.qweight.copy_(_dev(qw, cuda)); lin.qzeros.copy_(_dev(qz, cuda))
+    lin.scales.copy_(_dev(sc, cuda)); lin.bias.copy_(_dev(b, cuda))
+    lin.gemm_cfg = cfg
+    a = torch.randn((m, k), device=cuda).half()
+    stats = torch.zeros((m, k // 64, 2), device=cuda)
+    stats[..., 1] = 64.0                                   # unit variance per row
+    mu = torch.zeros(m, device=cuda)
+    gw, bw = lin.ln_fold_constants(torch.ones(k, device=cuda), torch.zeros(k, device=cuda))
+    out = torch.empty((m, n), dtype=torch.float16, device=cuda)
+    if ok:
+        lin.forward_lnf(a, ops.EPI_BIAS_LNF, out, stats, mu, gw=gw, bw=bw, eps=1e-6)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+    else:
+        with pytest.raises(NotImplementedError):
+            lin.forward_lnf(a, ops.EPI_BIAS_LNF, out, stats, mu, gw=gw, bw=bw, eps=1e-6)

@@ -200,3 +200,26 @@ def test_bench_in_step_gemm_classifier_on_committed_profiles():
         assert d["gemm_union_ns"] > 0, f.name
     assert bench.is_proj_gemm("w4a8", "void samq::i8_gemm_pp2<5, 3, 2, 8>(signed char const*, long)")
     assert not bench.is_proj_gemm("w8a8", "void samq::i8_gemm_pp2<5, 3, 2, 8>(signed char const*, long)")
+
+
+def test_bench_oracle_state_matches_test_oracle():
+    """bench.py's parity leg rebuilds the oracle from the bench encoder's own state dict
+    (``oracle_state``): on a small product encoder it must be the very oracle the GPU tests use
+    (oracle G1 from the same packed buffers), output for output."""
+    import sys
+    from pathlib import Path
+    import numpy as np
+    import torch
+    repo = Path(__file__).resolve().parent.parent
+    sys.path.insert(0, str(repo))
+    sys.path.insert(0, str(repo / "tests"))
+    import bench
+    from _encoder_helpers import oracle_g1, oracle_vith, product_encoder
+    from oracle import sam_ref, synth
+    cfg, st, names, q = oracle_vith(2, seed=3, name="vit_b", img_size=256, global_idx=(1,))
+    enc = product_encoder(cfg, st, names, q, -1, "cpu")
+    st2, lw, lb, _ = bench.oracle_state(enc, cfg, -1)
+    img = synth.make_images(1, 256, seed=4)
+    a = sam_ref.EncoderOracle(cfg, st2, linear_weights=lw, linear_bias=lb)(img).numpy()
+    b = oracle_g1(cfg, st, names, q)(img).numpy()
+    np.testing.assert_array_equal(a, b)

@@ -13,10 +13,11 @@ from oracle.w4a8_ref import W4A8EncoderOracle
 from _encoder_helpers import oracle_vith, product_encoder
 
 
-def _oracle(depth, seed, img_size=1024, name="vit_h", global_idx=None):
-    cfg, st, names, q = oracle_vith(depth, seed, name=name, img_size=img_size, global_idx=global_idx)
+def _oracle(depth, seed, img_size=1024, name="vit_h", global_idx=None, groupsize=-1):
+    cfg, st, names, q = oracle_vith(depth, seed, groupsize=groupsize, name=name, img_size=img_size,
+                                    global_idx=global_idx)
     from oracle import sam_ref
-    lw = sam_ref.quantized_linear_weights(q, names, -1)
+    lw = sam_ref.quantized_linear_weights(q, names, groupsize)
     lb = {n: q[n + ".bias"].astype(np.float32) for n in names}
     return cfg, st, names, q, W4A8EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb)
 
@@ -209,7 +210,8 @@ W4A8_ATTN_FRAC = 8e-3
 
 
 @pytest.mark.gpu
-def test_w4a8_stage_local_parity(cuda):
+@pytest.mark.parametrize("groupsize", [-1, 128])
+def test_w4a8_stage_local_parity(cuda, groupsize):
     """Each fused W4A8 stage, fed the W4A8 oracle's own inputs, reproduces the oracle's int8 codes
     (every code within +-1) or its float output (fp16 / fp32 rounding): the fp32 patch embedding;
     per block LN1 + quantiser; the qkv int4 x int8 GEMM + bias (fp16 out); the attention with its
@@ -217,11 +219,13 @@ def test_w4a8_stage_local_parity(cuda):
     residual.  ViT-H geometry at 1024^2, block 0 windowed (with the 64 -> 70 window padding),
     block 1 global.  Kernel-level code parity, the W4A8 counterpart of
     test_w8a8.py::test_w8a8_stage_local_parity; the reference halves are fq_vit QAct
-    (layers.py:203-242 / uniform.py:23-45) and the GPTQ W4 linear (quant_linear.py:292-343)."""
+    (layers.py:203-242 / uniform.py:23-45) and the GPTQ W4 linear (quant_linear.py:292-343).
+    groupsize 128: the grouped int4 weights on the int8 path (per-group exact int32 sums scaled in
+    f32, samq_w4a8_gemm_cfg; quant_linear.py:324-335) under the same bounds."""
     import samq
     from samq import ops
-    cfg, st, names, q, o = _oracle(2, 7, global_idx=(1,))
-    enc = product_encoder(cfg, st, names, q, -1, cuda).half()
+    cfg, st, names, q, o = _oracle(2, 7, global_idx=(1,), groupsize=groupsize)
+    enc = product_encoder(cfg, st, names, q, groupsize, cuda).half()
     samq.make_act_quant(enc)
     torch.set_num_threads(16)
     o.calibrate([synth.make_images(1, 1024, seed=1)])

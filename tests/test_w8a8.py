@@ -149,6 +149,57 @@ def test_w4a8_gemm_exact_integer(cuda, cfg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("groupsize,k", [(128, 1280), (256, 5120), (512, 1280)])
+@pytest.mark.parametrize("cfg", [0, 83, 84, 87, 88])
+def test_w4a8_gemm_grouped(cuda, groupsize, k, cfg):
+    """Grouped GPTQ weights on the int8 path (samq_w4a8_gemm_cfg; the reference applies per-group
+    scale / zero rows, quant_linear.py:324-335): per group g the int32 sum of a * (q - zp[g]) is
+    exact, scaled by s[g] in f32 and summed over the groups.  Reference: the exact integer group
+    sums in int64, combined in float64.  Groupsize 512 on K = 1280 leaves a half group at the end;
+    zero points include nibble 0 (quirk 4)."""
+    from oracle import gptq_pack
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(groupsize + k + cfg))
+    m, n = 333, 512
+    w = rng.standard_normal((n, k), dtype=np.float32) * np.float32(0.02)
+    w[7] = np.abs(w[7])
+    fake, s, z = gptq_pack.rtn_quantize_linear(w, groupsize)
+    qw, qz, sc = gptq_pack.pack_linear(fake, s, z, groupsize)
+    q = gptq_pack.unpack_qweight(qw).astype(np.int64)            # (K, N)
+    zp = gptq_pack.unpack_zeros(qz).astype(np.int64)             # (G, N)
+    scf = sc.astype(np.float32)                                  # (G, N)
+    a = rng.integers(-128, 128, (m, k), dtype=np.int8)
+    a_s = np.float32(0.013)
+    bias = (rng.standard_normal(n, dtype=np.float32) * 0.02).astype(np.float32)
+    y = np.zeros((m, n), np.float64)
+    for g in range(zp.shape[0]):
+        ks = slice(g * groupsize, min(k, (g + 1) * groupsize))
+        pg = a[:, ks].astype(np.int64) @ (q[ks] - zp[g][None, :])
+        y += pg.astype(np.float64) * scf[g].astype(np.float64)
+    y = y * np.float64(a_s) + bias
+    packed = ops.w4_repack(torch.from_numpy(qw).to(cuda), layout=3)
+    args = (torch.from_numpy(a).to(cuda), packed, torch.from_numpy(scf).to(cuda).reshape(-1).contiguous(),
+            torch.from_numpy(qz).to(cuda), n, torch.from_numpy(bias).to(cuda))
+    o32 = ops.w4a8_gemm(*args, ops.EPI_F32, float(a_s), groupsize=groupsize, cfg=cfg).cpu().numpy()
+    err = np.abs(o32 - y).max() / np.abs(y).max()
+    print(f"\n[w4a8 grouped] g={groupsize} K={k} cfg {cfg}: f32 max rel err {err:.2e}")
+    assert err <= 2e-6
+    o16 = ops.w4a8_gemm(*args, ops.EPI_BIAS, float(a_s), groupsize=groupsize, cfg=cfg)
+    assert np.abs(o16.float().cpu().numpy() - y).max() <= 1e-3 * max(1.0, np.abs(y).max())
+    # quantising GELU epilogue: codes of GELU(y) within one step (ties of the f32 value)
+    so = float(np.abs(y).max() / 100)
+    c8 = ops.w4a8_gemm(*args, ops.EPI_Q8_GELU, float(a_s), out_scale=so, groupsize=groupsize, cfg=cfg)
+    from oracle import sam_ref
+    ref8 = torch.clamp(torch.round(sam_ref.gelu_erf(torch.from_numpy(y).float()) / so), -128, 127).numpy()
+    d = np.abs(c8.cpu().numpy().astype(np.int64) - ref8.astype(np.int64))
+    assert d.max() <= 1 and (d > 0).mean() <= 1e-3
+    # per-channel weights (G = 1) through the same entry point stay on the per-channel kernels
+    if cfg == 0:
+        with pytest.raises(NotImplementedError):
+            ops.w4a8_gemm(*args, ops.EPI_F32, float(a_s), groupsize=64)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("m,k,n", [(300, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280), (77, 128, 256),
                                    (260, 256, 768)])
 @pytest.mark.parametrize("cfg", [85, 86])

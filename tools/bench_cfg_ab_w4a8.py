@@ -16,7 +16,8 @@ dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 VARIANTS = {"pick": {}, "all=86": {"qkv": 86, "proj": 86, "lin1": 86, "lin2": 86},
-            "all=81": {"qkv": 81, "proj": 81, "lin1": 81, "lin2": 81}}
+            "all=81": {"qkv": 81, "proj": 81, "lin1": 81, "lin2": 81},
+            "all=93": {"qkv": 93, "proj": 93, "lin1": 93, "lin2": 93}}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 enc.half()

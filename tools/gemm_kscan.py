@@ -17,7 +17,7 @@ cfgs = [int(c) for c in (sys.argv[2] if len(sys.argv) > 2 else "22").split(",")]
 for n, epi in ((3840, ops.EPI_BIAS), (1280, ops.EPI_RESADD_F32)):
     for cfg in cfgs:
         pts = []
-        for k in (640, 1280, 2560, 5120):
+        for k in ([int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else (640, 1280, 2560, 5120)):
             q = QuantLinear(4, -1, k, n, True).to(dev)
             fake, s, z = rtn(torch.randn(n, k, device=dev) * 0.02)
             pack_linear(q, fake, s, z, torch.randn(n, device=dev) * 0.02)
