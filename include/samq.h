@@ -245,6 +245,14 @@ int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* be
                      int C, float eps, int flags, float in_scale, float out_scale,
                      hipStream_t stream);
 
+/* Residual add + LayerNorm (Block.forward's x = x + attn(...) / x = x + mlp(...) followed by the
+ * next norm, image_encoder.py:199-207): x f32 [rows, C] += delta (f16 with SAMQ_LN_DELTA_F16,
+ * else f32 -- the preceding GEMM's plain-stored output), written back in place, then
+ * y = LayerNorm(x) (f16, or int8 codes q(LN(x), out_scale) with SAMQ_LN_OUT_I8).  C <= 1280. */
+#define SAMQ_LN_DELTA_F16 16
+int samq_add_layernorm(void* x, const void* delta, void* y, const float* gamma, const float* beta,
+                       int64_t rows, int C, float eps, int flags, float out_scale, hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention */
 
 /* Multi-head attention with in-kernel decomposed relative-position bias over an image token

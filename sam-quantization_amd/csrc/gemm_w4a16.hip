@@ -1121,6 +1121,52 @@ __device__ __forceinline__ void te_store4(const float4_t& acc, const float4_t& s
   }
 }
 
+// Staged epilogue of TRANSPOSED 32x32 accumulators (VAR & 65536), f16 outputs: lane (l32, hsel) of
+// tile (i, t) holds row 32 i + l32, columns 32 t + 8 j + 4 hsel .. +3 in register group j, so four
+// consecutive columns convert to one 8-byte f16 group -> ONE ds_write_b64 per 4 values (the
+// row-pitch 144 B keeps the 16 rows of a write group on distinct banks), then row-contiguous
+// ds_read_b128 + 16-byte global stores.  The whole WM x WN wave tile is staged at once in the LDS
+// the ring frees (f16: 18 KiB per wave).  vs pp_epilogue: 4x fewer LDS write instructions and half
+// the staged bytes (f16 instead of f32).
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void te_staged_epilogue_f16(const float16_t (&acc)[TM][TN], const _Float16* __restrict__ scales,
+                                                       const _Float16* __restrict__ bias, char* ep, void* Cout,
+                                                       int64_t ldc, int M, int row_base, int col_base, int lane) {
+  static_assert(EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU, "f16 outputs");
+  constexpr int WN = TN * 32, PITCH = WN * 2 + 16, C8 = WN / 8;
+  const int l32 = lane & 31, hsel = lane >> 5;
+#pragma unroll
+  for (int t = 0; t < TN; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = 32 * t + 8 * j + 4 * hsel;
+      const half4_t s4 = *(const half4_t*)(scales + col_base + cl);
+      const half4_t b4 = bias ? *(const half4_t*)(bias + col_base + cl) : half4_t{0, 0, 0, 0};
+      const float2_t sa = {(float)s4[0], (float)s4[1]}, sb = {(float)s4[2], (float)s4[3]};
+      const float2_t ba = {(float)b4[0], (float)b4[1]}, bb = {(float)b4[2], (float)b4[3]};
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float2_t v0 = __builtin_elementwise_fma((float2_t){acc[i][t][4 * j], acc[i][t][4 * j + 1]}, sa, ba);
+        float2_t v1 = __builtin_elementwise_fma((float2_t){acc[i][t][4 * j + 2], acc[i][t][4 * j + 3]}, sb, bb);
+        if (EPI == SAMQ_EPI_BIAS_GELU) {
+          v0 = gelu_fast2(v0);
+          v1 = gelu_fast2(v1);
+        }
+        const half2_t h0 = __builtin_convertvector(v0, half2_t), h1 = __builtin_convertvector(v1, half2_t);
+        *(half4_t*)(ep + (32 * i + l32) * PITCH + cl * 2) = half4_t{h0.x, h0.y, h1.x, h1.y};
+      }
+    }
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the wave's own tile is in LDS
+#pragma unroll
+  for (int it = 0; it < TM * 32 * C8 / 64; ++it) {
+    const int idx = it * 64 + lane;
+    const int rl = idx / C8, c8 = idx % C8;
+    const half8_t h = *(const half8_t*)(ep + rl * PITCH + c8 * 16);
+    const int row = row_base + rl;
+    if (row < M) *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
+  }
+}
+
 // ------------------------------------------------------------------ GEMM v6 (ping-pong, k-phases)
 // As v5, but a phase is a K-PART of the tile over ALL of the wave's output tiles: phase p
 // multiplies k16-steps [p*KPP, (p+1)*KPP) for TM x TN accumulators, so every phase reads its own
@@ -1225,7 +1271,11 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   // VAR & 16: v_mfma_f32_16x16x32_f16 fragments (same tile, LDS bytes and unpack count; the chip
   // holds a higher clock on this shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7)
   constexpr bool M16 = (VAR & 16) != 0;
-  constexpr bool TE = (VAR & 128) != 0;   // transposed accumulators + direct epilogue (te_store4)
+  // VAR & 65536: transposed accumulators + the LDS-staged f16 epilogue (te_staged_epilogue_f16)
+  constexpr bool TES = (VAR & 65536) != 0;
+  static_assert(!TES || (!M16 && !GR && (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU)), "TES: f16 outputs, 32x32");
+  static_assert(!TES || 8 * TM * 32 * (TN * 64 + 16) <= 163840, "TES staging");
+  constexpr bool TE = (VAR & 128) != 0 || TES;   // transposed accumulators (+ direct epilogue te_store4)
   // VAR & 16384: LDS-DMA pieces spread through the MFMA burst (see the MFMA half)
   constexpr bool DMA_SPREAD = (VAR & 16384) != 0;
   static_assert(!DMA_SPREAD || !(DMA_LOAD || TE || (VAR & 2)), "DMA spread: product MFMA halves only");
@@ -1615,6 +1665,13 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       }
     return;
   }
+  if constexpr (TES) {
+    constexpr int WB = TM * 32 * (TN * 64 + 16);
+    __syncthreads();   // every wave is done with the ring
+    te_staged_epilogue_f16<TM, TN, EPI>(acc, scales, bias, smem + wave * WB, Cout, ldc, M, m0 + wm * WM, n0 + wn * WN,
+                                        lane);
+    return;
+  }
   if constexpr (!M16 && TE) {
     // lane (l32, hsel) holds row 32 i + l32, columns 32 t + 8 j + 4 hsel .. +3 in register group j
 #pragma unroll
@@ -1763,6 +1820,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
       // cfg 57 / 64 with the LDS-DMA pieces spread through the MFMA burst (VAR & 16384)
       case 100: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 16384>(a, st);
+      // cfg 57 with transposed accumulators and the f16-staged epilogue (f16 outputs only)
+      case 104:
+        if constexpr (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 65536>(a, st);
+        else return fail(SAMQ_ERR_INVALID, "w4a16_gemm: cfg 104 has f16 epilogues (BIAS / BIAS_GELU) only");
       case 101: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 16384>(a, st);
 #ifdef SAMQ_TUNING
       // tuning build only (make tuning): untested shapes and TIMING-ONLY variants that compute
@@ -1905,7 +1966,7 @@ static int cfg_bn(int cfg) {
                  case 74: case 75: case 76: case 77: case 78: case 79: return 256;
                  case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
                  case 97: case 98: return 512;
-                 case 100: case 101: case 102: case 103: return 256;
+                 case 100: case 101: case 102: case 103: case 104: return 256;
                  default: return 0; }
 }
 

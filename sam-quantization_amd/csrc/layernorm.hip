@@ -14,12 +14,18 @@ __device__ __forceinline__ float ln_q8(float v, float s) {   // fq_vit uniform.p
   return q8_exact(v, s, 1.0f / s);   // the reciprocal is loop-invariant (hoisted)
 }
 
-template <int IN, int OUT, int VPT, int RPW>  // VPT = 4-channel vectors per lane, RPW = rows per wave
+// ADD (f32 input only): the residual add of the GEMM before the LayerNorm runs here instead of in
+// that GEMM's epilogue -- x += delta (delta f16 when ADD == 1, f32 when ADD == 2; the GEMM wrote
+// y = acc * s + b with a plain store), x written back in place, then the LayerNorm of the new x.
+// f32 delta: the same fp32 add as the GEMM's read-modify-write epilogue (bit-identical x).
+template <int IN, int OUT, int VPT, int RPW, int ADD = 0>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ xin, void* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows, int C,
                                                         float eps, float in_scale, float out_scale,
-                                                        float* __restrict__ mean_out) {
+                                                        float* __restrict__ mean_out,
+                                                        const void* __restrict__ delta = nullptr) {
+  static_assert(ADD == 0 || IN == LN_F32, "residual add: f32 rows");
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   if (row0 >= rows) return;
@@ -42,9 +48,28 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
           for (int e = 0; e < 4; ++e) v[r][i][e] = (float)(int8_t)((w >> (8 * e)) & 0xFFu) * in_scale;
         } else {
           v[r][i] = ((const float4_t*)xin)[row * nvec + j];
+          if constexpr (ADD == 1) {
+            const half4_t h = ((const half4_t*)delta)[row * nvec + j];
+            v[r][i] += float4_t{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+          } else if constexpr (ADD == 2) {
+            v[r][i] += ((const float4_t*)delta)[row * nvec + j];
+          }
         }
       } else {
         v[r][i] = float4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  if constexpr (ADD != 0) {   // the new residual rows back in place
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int64_t row = row0 + r;
+      if (row < rows) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+          const int j = lane + 64 * i;
+          if (j < nvec) ((float4_t*)xin)[row * nvec + j] = v[r][i];
+        }
       }
     }
   }
@@ -170,6 +195,33 @@ extern "C" int samq_layernorm_mean(const void* x, void* y, const float* gamma, c
   SAMQ_REQUIRE(mean_out, SAMQ_ERR_INVALID, "layernorm_mean: null mean_out");
   return ln_launch(x, y, gamma, beta, rows, C, eps, (flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32,
                    (flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16, 1.f, 1.f, ln_rpw(flags), stream, mean_out);
+}
+
+// x += delta (f16 [rows, C] with SAMQ_LN_DELTA_F16, else f32), in place, then y = LN(x) (f16, or
+// int8 codes q(LN(x), out_scale) with SAMQ_LN_OUT_I8): the residual add of the preceding GEMM
+// moved out of its epilogue.  Rows of C <= 1280 (the ViT-H / vit_b widths).
+extern "C" int samq_add_layernorm(void* x, const void* delta, void* y, const float* gamma, const float* beta,
+                                  int64_t rows, int C, float eps, int flags, float out_scale, hipStream_t stream) {
+  SAMQ_REQUIRE(x && delta && y && gamma && beta, SAMQ_ERR_INVALID, "add_layernorm: null pointer");
+  SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 1280, SAMQ_ERR_INVALID, "add_layernorm: C must be a multiple of 4, <= 1280");
+  SAMQ_REQUIRE(!(flags & SAMQ_LN_OUT_I8) || out_scale > 0.f, SAMQ_ERR_INVALID, "add_layernorm: out_scale must be > 0");
+  if (rows <= 0) return SAMQ_OK;
+  const int rpw = ln_rpw(flags);
+  SAMQ_REQUIRE(rpw == 1 || rpw == 2 || rpw == 4, SAMQ_ERR_INVALID, "add_layernorm: rows per wave must be 1, 2 or 4");
+  const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
+  const bool i8 = (flags & SAMQ_LN_OUT_I8) != 0, d16 = (flags & SAMQ_LN_DELTA_F16) != 0;
+  const int vpt = (C / 4 + 63) / 64;
+#define ALN(O, V, R, A) hipLaunchKernelGGL((layernorm_kernel<LN_F32, O, V, R, A>), grid, dim3(256), 0, stream, x, y, gamma, \
+                                           beta, rows, C, eps, 1.f, out_scale, nullptr, delta)
+#define ALN_R(O, V, A) do { if (rpw == 1) ALN(O, V, 1, A); else if (rpw == 2) ALN(O, V, 2, A); else ALN(O, V, 4, A); } while (0)
+#define ALN_V(O, A) do { if (vpt <= 3) ALN_R(O, 3, A); else if (vpt <= 4) ALN_R(O, 4, A); else ALN_R(O, 5, A); } while (0)
+  if (i8) { if (d16) ALN_V(LN_I8, 1); else ALN_V(LN_I8, 2); }
+  else { if (d16) ALN_V(LN_F16, 1); else ALN_V(LN_F16, 2); }
+#undef ALN_V
+#undef ALN_R
+#undef ALN
+  SAMQ_LAUNCH_CHECK("add_layernorm launch");
+  return SAMQ_OK;
 }
 
 extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,

@@ -45,6 +45,7 @@ LN_IN_F16 = 1
 LN_OUT_F32 = 2
 LN_IN_I8 = 4
 LN_OUT_I8 = 8
+LN_DELTA_F16 = 16
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int
@@ -73,6 +74,7 @@ SIGNATURES = {
                                 _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "samq_w8a8_conv_gemm": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
                                    _f32, _f32, _f32, _f32, _vp]),
+    "samq_add_layernorm": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _vp]),
     "samq_quantize": (_i32, [_vp, _vp, _i64, _f32, _i32, _vp]),
     "samq_minmax_workspace": (ctypes.c_size_t, [_i64, _i32, _i32]),
     "samq_minmax": (_i32, [_vp, _i64, _i32, _i32, _i32, _vp, _vp, _i32, _vp, ctypes.c_size_t, _vp]),

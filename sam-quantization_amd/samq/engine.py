@@ -55,6 +55,10 @@ class EncoderEngine:
         # lanes > 1: lane i+1 starts after lane i's launch number ``lane_stagger`` (7 per block,
         # block 0 first; -1 = all lanes start together) -- an in-graph A/B knob
         self.lane_stagger = 1   # measured: +0.3 % over no stagger (profiles/r3_v9_lane_stagger.log)
+        # where the residual adds of proj / lin2 run: "epi" = the GEMM's read-modify-write epilogue
+        # (x += y in f32); "ln32" = the GEMM stores y (f32) and the next LayerNorm adds it
+        # (samq_add_layernorm, bit-identical x); "ln16" = the same with y stored as f16
+        self.res_mode = "epi"
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
@@ -191,25 +195,40 @@ class EncoderEngine:
             return
         ops.patch_embed(img.to(torch.float32).contiguous(), self.pe_w32, self.pe_b, pos, p, out=x32)
 
-    def block_w4a8(self, p: _BlockPlan, bufs, mark=None) -> None:
+    def block_w4a8(self, p: _BlockPlan, bufs, mark=None, first: bool = True, last: bool = True) -> None:
         """W4A8 block: int8 codes into every GEMM (fq_vit QAct on each QuantLinear input, folded
-        into LN / the GELU epilogue / the attention's store), int8 MFMA GEMMs.  ``mark(k)`` as in
-        ``block``."""
+        into LN / the GELU epilogue / the attention's store), int8 MFMA GEMMs.  ``mark(k)``,
+        ``first`` / ``last`` and ``res_mode`` as in ``block`` ("ln16" stores f32 deltas here too:
+        the int8 GEMMs have no f16 residual output)."""
         mark = mark or (lambda k: None)
         x, xn8, qkv, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att8"], bufs["hid8"]
-        ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
+        late = self.res_mode != "epi"
+        if late and not first:
+            ops.add_layernorm(x, self._delta(bufs, torch.float32), p.ln1_w, p.ln1_b, p.ln1_eps, out=xn8,
+                              out_scale=p.s_qkv)
+        else:
+            ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
         mark(0)
         p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
         mark(1)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8, out_scale=p.s_proj)
         mark(2)
-        p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
-        mark(3)
-        ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
+        if late:
+            p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_F32, out=self._delta(bufs, torch.float32))
+            mark(3)
+            ops.add_layernorm(x, self._delta(bufs, torch.float32), p.ln2_w, p.ln2_b, p.ln2_eps, out=xn8,
+                              out_scale=p.s_lin1)
+        else:
+            p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
+            mark(3)
+            ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
         mark(4)
         p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
         mark(5)
-        p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
+        if late and not last:
+            p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_F32, out=self._delta(bufs, torch.float32))
+        else:
+            p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
         mark(6)
 
     # ---------------------------------------------------------------- LayerNorm fold
@@ -264,25 +283,54 @@ class EncoderEngine:
             p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
         mark(6)
 
-    def block(self, p: _BlockPlan, bufs, mark=None) -> None:
-        """One W4A16 block (7 launches).  ``mark(k)`` (lane stagger) runs after launch k."""
+    def _delta(self, bufs, dtype=None) -> torch.Tensor:
+        """The proj / lin2 output the next LayerNorm adds to x (res_mode "ln32": f32, "ln16": f16),
+        allocated with the lane's buffers on first use."""
+        dtype = dtype or (torch.float16 if self.res_mode == "ln16" else torch.float32)
+        key = "delta16" if dtype == torch.float16 else "delta32"
+        t = bufs.get(key)
+        if t is None:
+            t = bufs[key] = torch.empty(bufs["x"].shape, dtype=dtype, device=bufs["x"].device)
+        return t
+
+    def _res_add_ln(self, x, bufs, w, b, eps, out, pending: bool) -> None:
+        """The LayerNorm in front of a block half; with ``pending`` (res_mode != "epi") the
+        preceding GEMM's output (``_delta``) is first added to x (samq_add_layernorm)."""
+        if pending:
+            ops.add_layernorm(x, self._delta(bufs), w, b, eps, out=out, rows_per_wave=self.ln_rpw)
+        else:
+            ops.layernorm(x, w, b, eps, out=out, rows_per_wave=self.ln_rpw)
+
+    def block(self, p: _BlockPlan, bufs, mark=None, first: bool = True, last: bool = True) -> None:
+        """One W4A16 block (7 launches).  ``mark(k)`` (lane stagger) runs after launch k.  With
+        ``res_mode`` "ln32" / "ln16" the residual adds run in the LayerNorms: proj and lin2 store
+        y into ``delta`` and the next LayerNorm adds it (``first``: x is complete on entry; ``last``:
+        lin2 adds in its own epilogue so x is complete for the neck)."""
         if self.w4a8:
-            return self.block_w4a8(p, bufs, mark)
+            return self.block_w4a8(p, bufs, mark, first, last)
         mark = mark or (lambda k: None)
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
-        ops.layernorm(x, p.ln1_w, p.ln1_b, p.ln1_eps, out=xn, rows_per_wave=self.ln_rpw)
+        late = self.res_mode != "epi"
+        res_epi = ops.EPI_BIAS if self.res_mode == "ln16" else ops.EPI_F32
+        self._res_add_ln(x, bufs, p.ln1_w, p.ln1_b, p.ln1_eps, xn, late and not first)
         mark(0)
         p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
         mark(1)
         ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
         mark(2)
-        p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
+        if late:
+            p.proj.forward_epilogue(att, res_epi, out=self._delta(bufs))
+        else:
+            p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
         mark(3)
-        ops.layernorm(x, p.ln2_w, p.ln2_b, p.ln2_eps, out=xn, rows_per_wave=self.ln_rpw)
+        self._res_add_ln(x, bufs, p.ln2_w, p.ln2_b, p.ln2_eps, xn, late)
         mark(4)
         p.lin1.forward_epilogue(xn, ops.EPI_BIAS_GELU, out=hid)
         mark(5)
-        p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
+        if late and not last:
+            p.lin2.forward_epilogue(hid, res_epi, out=self._delta(bufs))
+        else:
+            p.lin2.forward_epilogue(hid, ops.EPI_RESADD_F32, out=x)
         mark(6)
 
     def neck(self, x32: torch.Tensor, out_dtype) -> torch.Tensor:
@@ -363,7 +411,7 @@ class EncoderEngine:
             if fold:
                 self.block_fold(i, bufs, mark)
             else:
-                self.block(p, bufs, mark)
+                self.block(p, bufs, mark, first=i == 0, last=i + 1 == len(self.plans))
         if gate_event is not None and self.lane_stagger // 7 >= len(self.plans):
             gate_event.record()
         return self.neck(bufs["x"], out_dtype)
@@ -375,8 +423,9 @@ class EncoderEngine:
         """fp32 residual stream after ``upto`` blocks (debug / parity helper)."""
         bufs = self.buffers(img.shape[0])
         self.embed(img, bufs["x"])
-        for p in self.plans[: (len(self.plans) if upto is None else upto)]:
-            self.block(p, bufs)
+        n = len(self.plans) if upto is None else upto
+        for i, p in enumerate(self.plans[:n]):
+            self.block(p, bufs, first=i == 0, last=i + 1 == n)
         return bufs["x"].clone()
 
     def capture(self, img_static: torch.Tensor, out_dtype=None, lanes: int = 1):

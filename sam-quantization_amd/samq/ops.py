@@ -23,7 +23,7 @@ EPI_BIAS_LNF = _lib.EPI_BIAS_LNF
 EPI_GELU_LNF = _lib.EPI_GELU_LNF
 
 # W4A16 tile configs of the product library (include/samq.h, samq_w4a16_gemm_cfg); 0 = automatic
-W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65, 100, 101))
+W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65, 100, 101, 104))
 _Q8_EPIS = (EPI_Q8, EPI_Q8_GELU, EPI_Q8_RES)
 
 
@@ -169,6 +169,27 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
         return out
     _lib.check(_lib.load().samq_layernorm(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), rows, c, float(eps), flags,
                                           _stream()), "layernorm")
+    return out
+
+
+def add_layernorm(x: torch.Tensor, delta: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-6,
+                  out: Optional[torch.Tensor] = None, out_scale: float = 0.0, rows_per_wave: int = 0) -> torch.Tensor:
+    """x (f32, in place) += delta (f16 or f32, same shape); returns LayerNorm(x) as f16, or as int8
+    codes q(LN(x), out_scale) when ``out`` is int8 (samq_add_layernorm: the residual add of the
+    preceding GEMM moved out of its epilogue)."""
+    _need_cuda(x, delta, gamma, beta)
+    c = x.shape[-1]
+    assert x.is_contiguous() and x.dtype == torch.float32 and delta.is_contiguous()
+    assert delta.dtype in (torch.float16, torch.float32) and delta.numel() == x.numel()
+    assert gamma.dtype == torch.float32 and beta.dtype == torch.float32
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.int8 if out_scale > 0 else torch.float16, device=x.device)
+    assert out.is_contiguous() and out.dtype in (torch.float16, torch.int8) and out.numel() == x.numel()
+    flags = (_lib.LN_DELTA_F16 if delta.dtype == torch.float16 else 0) | (_lib.LN_OUT_I8 if out.dtype == torch.int8
+                                                                           else 0)
+    flags |= rows_per_wave << 16
+    _lib.check(_lib.load().samq_add_layernorm(_ptr(x), _ptr(delta), _ptr(out), _ptr(gamma), _ptr(beta), x.numel() // c,
+                                              c, float(eps), flags, float(out_scale), _stream()), "add_layernorm")
     return out
 
 

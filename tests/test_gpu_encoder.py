@@ -83,6 +83,37 @@ def test_batch_and_graph_consistency(cuda, vith32):
     assert torch.isfinite(out).all()
 
 
+@pytest.mark.parametrize("res_mode", ["ln32", "ln16"])
+def test_residual_add_in_layernorm(cuda, vith32, res_mode):
+    """engine.res_mode: the proj / lin2 residual adds moved from the GEMM epilogue into the next
+    LayerNorm (samq_add_layernorm).  "ln32" stores the f32 GEMM output and adds it with the same
+    f32 add: bit-identical to the epilogue form.  "ln16" stores it as f16 (the reference's fp16
+    model stores every activation in fp16): within the north-star tolerance of oracle G1."""
+    cfg, st, names, q, enc, img, _ = vith32
+    eng = enc.engine()
+    x = torch.from_numpy(img).to(cuda)
+    x2 = torch.cat([x, torch.flip(x, dims=[-1])])
+    ref = eng(x2, out_dtype=torch.float32, lanes=2)
+    eng.res_mode = res_mode
+    try:
+        out = eng(x2, out_dtype=torch.float32, lanes=2)
+        static = x2.clone()
+        graph, gout = eng.capture(static, out_dtype=torch.float32, lanes=2)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(gout, out)
+    finally:
+        eng.res_mode = "epi"
+    if res_mode == "ln32":
+        assert torch.equal(out, ref)
+    else:
+        torch.set_num_threads(16)
+        g1 = oracle_g1(cfg, st, names, q)(img).numpy()
+        err = _report("vit_h 32 blocks engine (residual adds in the LayerNorms, f16 deltas) vs oracle G1",
+                      out[:1].cpu().numpy(), g1)
+        assert err <= TOL
+
+
 @pytest.mark.parametrize("lanes", [2, 4])
 def test_lanes_bit_identical(cuda, vith32, lanes):
     """Image groups on concurrent HIP streams (engine.forward ``lanes``), eager and captured,

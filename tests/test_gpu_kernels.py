@@ -98,12 +98,15 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
         _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
 
 
-@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101])
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101, 104])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
-    ragged M, short and long K (1 .. 40 K tiles, so the ring prologue / retire paths all run)."""
+    ragged M, short and long K (1 .. 40 K tiles, so the ring prologue / retire paths all run).
+    cfg 104 (transposed accumulators, f16-staged epilogue) has the f16 epilogues only."""
     from samq import ops
+    if cfg == 104 and epi in ("resadd", "f32"):
+        pytest.skip("cfg 104: f16 epilogues only")
     for m, k, n in ((333, 1280, 512), (300, 64, 256), (260, 192, 256), (513, 2560, 768)):
         qw, qz, sc, bias = _packed_layer(k, n, -1, seed=cfg * 13 + k)
         rng = np.random.Generator(np.random.PCG64(cfg + k))
@@ -208,6 +211,34 @@ def test_layernorm(cuda, c, in_dtype, rpw):
     _close(out32, ref, 2e-5)
 
 
+@pytest.mark.parametrize("c", [768, 1280])
+@pytest.mark.parametrize("delta_dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("q8", [False, True])
+def test_add_layernorm(cuda, c, delta_dtype, q8):
+    """samq_add_layernorm: x += delta in place (bit-identical to the f32 add of the GEMM's
+    residual epilogue), then LayerNorm(x) as f16 or as int8 codes (fq_vit quantiser)."""
+    from samq import ops
+    g = torch.Generator().manual_seed(c + q8)
+    x = torch.randn(1003, c, generator=g) * 3 + 1.5
+    d = (torch.randn(1003, c, generator=g) * 0.7).to(delta_dtype)
+    w = 1 + 0.1 * torch.randn(c, generator=g)
+    b = 0.1 * torch.randn(c, generator=g)
+    xs = x + d.float()
+    ref = torch.nn.functional.layer_norm(xs, (c,), w, b, eps=1e-6)
+    xd = x.to(cuda)
+    if q8:
+        s = 0.03
+        out = ops.add_layernorm(xd, d.to(cuda), w.to(cuda), b.to(cuda), 1e-6, out_scale=s)
+        codes = torch.clamp(torch.round(ref / s), -128, 127)
+        diff = (out.cpu().to(torch.int64) - codes.to(torch.int64)).abs()
+        assert out.dtype == torch.int8 and int(diff.max()) <= 1 and float((diff > 0).double().mean()) < 1e-3
+    else:
+        out = ops.add_layernorm(xd, d.to(cuda), w.to(cuda), b.to(cuda), 1e-6)
+        _close(out, ref.numpy(), 1.5e-3)
+    torch.cuda.synchronize()
+    assert torch.equal(xd.cpu(), xs)
+
+
 def _attn_case(b, h, w, heads, d, window, seed):
     rng = np.random.Generator(np.random.PCG64(seed))
     c = heads * d
@@ -265,20 +296,26 @@ def test_rel_attention(cuda, b, h, w, heads, d, window):
     (3, 16, 16, 2, 80, 0),      # resident small global grid
 ])
 def test_rel_attention_q_out(cuda, b, h, w, heads, d, window):
-    """samq_rel_attention_q (the W4A8 proj-input QAct folded into the attention store) is BIT-IDENTICAL
-    to samq_rel_attention followed by samq_quantize, and the codes match the oracle's fake quant up
-    to the fp16 rounding of the attention output (+-1 code)."""
+    """samq_rel_attention_q (the W4A8 proj-input QAct folded into the attention store) quantises the
+    f32 attention output itself (round 4; round 3 quantised its fp16 rounding, bit-identical to
+    samq_rel_attention + samq_quantize): against that fp16 composition every code is within one
+    step, and against the oracle's fake quant of its f32 attention the codes are within one step
+    and no further off than the fp16 composition's."""
     from samq import ops
     qkv16, bq, rph, rpw, ref = _attn_case(b, h, w, heads, d, window, seed=7 + h + window)
     args = (_dev(qkv16, cuda), _dev(bq, cuda), _dev(rph, cuda), _dev(rpw, cuda), heads, window, d ** -0.5)
     s = 0.011
     o16 = ops.rel_attention(*args)
-    want = ops.quantize(o16, s)
+    via16 = ops.quantize(o16, s).cpu().numpy().astype(np.int32)
     got = ops.rel_attention(*args, out_scale=s)
     torch.cuda.synchronize()
-    assert got.dtype == torch.int8 and torch.equal(got, want)
+    assert got.dtype == torch.int8
+    got = got.cpu().numpy().astype(np.int32)
+    assert np.abs(got - via16).max() <= 1
     codes = np.clip(np.rint(ref / np.float32(s)), -128, 127)
-    assert np.abs(got.cpu().numpy().astype(np.int32) - codes).max() <= 1
+    f_got, f_16 = float((got != codes).mean()), float((via16 != codes).mean())
+    print(f"\n[attn q8] codes off by one vs oracle: f32 store {f_got:.2e}, via fp16 {f_16:.2e}")
+    assert np.abs(got - codes).max() <= 1 and f_got <= f_16 + 1e-4
 
 
 @pytest.mark.parametrize("s,d", [(64, 80), (32, 64)])

@@ -49,7 +49,7 @@ def test_c_abi_rejects_timing_and_layout2_configs():
     from samq.quant_linear import QuantLinear
     lib = _lib.load()
     p = ctypes.c_void_p(4096)
-    for cfg in range(1, 100):
+    for cfg in range(1, 120):
         if cfg in ops.W4A16_CFGS:
             continue
         st = lib.samq_w4a16_gemm_cfg(p, 1280, p, p, p, None, p, 1280, 256, 1280, 1280, -1, 0, cfg, None)

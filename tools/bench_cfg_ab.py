@@ -20,7 +20,8 @@ if len(sys.argv) > 3:   # variants as "name:layer=cfg,layer=cfg;name:..." (pick 
     VARIANTS = {"pick": {}}
     for v in sys.argv[3].split(";"):
         name, spec = v.split(":")
-        VARIANTS[name] = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in spec.split(",")}
+        VARIANTS[name] = {kv.split("=")[0]: (kv.split("=")[1] if kv.split("=")[0] == "res" else int(kv.split("=")[1]))
+                          for kv in spec.split(",")}
 
 import os  # noqa: E402
 enc = random_quant_encoder("vit_h", int(os.environ.get("SAMQ_AB_GS", "-1")), device=dev)   # groupsize
@@ -30,6 +31,7 @@ img = torch.randn((4, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.ln_rpw = cfg.get("ln_rpw", 0)
+    eng.res_mode = cfg.get("res", "epi")   # where the proj / lin2 residual adds run (engine.res_mode)
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).gemm_cfg = cfg.get(lay, 0)
@@ -37,10 +39,10 @@ for name, cfg in VARIANTS.items():
     graph.replay()
     torch.cuda.synchronize()
     ref = out.clone() if ref is None else ref
-    graphs[name] = (graph, torch.equal(out, ref))
+    graphs[name] = (graph, torch.equal(out, ref), float((out.float() - ref.float()).abs().max()))
 times = {k: [] for k in graphs}
 for _ in range(rounds):
-    for name, (graph, _) in graphs.items():
+    for name, (graph, *_) in graphs.items():
         for _ in range(3):
             graph.replay()
         torch.cuda.synchronize()
@@ -52,4 +54,5 @@ for _ in range(rounds):
 for name, ts in times.items():
     ts.sort()
     print(f"lanes={lanes} {name:16s} median {ts[len(ts) // 2]:.3f} ms/step  min {ts[0]:.3f}  "
-          f"({4 / ts[len(ts) // 2] * 1e3:.1f} img/s)  bit-identical: {graphs[name][1]}", flush=True)
+          f"({4 / ts[len(ts) // 2] * 1e3:.1f} img/s)  bit-identical: {graphs[name][1]} "
+          f"(max-abs vs pick {graphs[name][2]:.2e})", flush=True)

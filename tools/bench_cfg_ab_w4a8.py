@@ -15,9 +15,7 @@ from samq.synthetic import random_quant_encoder  # noqa: E402
 dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
-VARIANTS = {"pick": {}, "all=86": {"qkv": 86, "proj": 86, "lin1": 86, "lin2": 86},
-            "all=81": {"qkv": 81, "proj": 81, "lin1": 81, "lin2": 81},
-            "all=93": {"qkv": 93, "proj": 93, "lin1": 93, "lin2": 93}}
+VARIANTS = {"pick": {}, "res=ln32": {"res": "ln32"}}   # round 4: residual adds in the LayerNorm-q kernels
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 enc.half()
@@ -29,6 +27,7 @@ g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((8, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
+    eng.res_mode = cfg.get("res", "epi")
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).i8_cfg = cfg.get(lay, 0)
