@@ -857,7 +857,8 @@ __device__ unsigned long long g_attn_stamps[8];   // timing experiments (tuning 
 #endif
 
 // DBG (tuning build only): & 1 per-wave s_memtime stamps of the four loop segments; & 2 no exp2,
-// & 4 no MFMAs (timing-only variants, wrong results)
+// & 4 no MFMAs (timing-only variants, wrong results); & 8 the softmax offset folded into the
+// Q.K^T C input (COFF below)
 template <int DBG>
 __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) {
   constexpr int D = 80, S = 64, KS = 5;
@@ -867,6 +868,10 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   constexpr int THB = 64 * 32 * 2;                // per wave: fp16 TH[kh][q]
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 8 * THB];
   constexpr bool DBG_NOEXP = (DBG & 2) != 0, DBG_NOMFMA = (DBG & 4) != 0;
+  // COFF: the next row's TH and softmax offset enter its Q.K^T as part of the C input
+  // (C = TW + (TH[kh] - offset), a per-lane scalar added in the MFMA segment), so the softmax
+  // segment -- the longer of the two -- runs exp2 straight on the scores (32 fewer v_sub per row)
+  constexpr bool COFF = (DBG & 8) != 0;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
 
@@ -984,10 +989,12 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
 #pragma unroll
       for (int s = 0; s < KS; ++s) kf[kt][s] = *(const half8_t*)(kb + (kt * 5 + s) * 1024 + lane * 16);
   };
-  auto qk = [&]() {   // S^T = K . Q^T + TW for the two 32-key tiles of a key row
+  float coff = 0.f;   // COFF: TH of the next row minus the offset baked into its scores
+  auto qk = [&]() {   // S^T = K . Q^T + TW (COFF: + coff) for the two 32-key tiles of a key row
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       float16_t a = tw[kt];
+      if constexpr (COFF) a = a + coff;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (DBG_NOMFMA) a[s] += (float)kf[kt][s][0] * (float)qf[s][0];
@@ -1006,7 +1013,63 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   float th_cur = (float)thw[l32];   // TH of row 0
   float m_pend = -INFINITY;
   bool pend = false;
+  // COFF: moff = the offset baked into the current row's scores (m after the pending move, 0 for
+  // row 0 whose m is -inf); the scores are then s + TH - moff and P = exp2(score)
+  float moff = 0.f;
+  if constexpr (COFF) coff = th_cur;
+  auto softmax_coff = [&](int kh) {
+    if (__any(pend)) {   // last row's deferred offset move (moff already includes it)
+      const float alpha = pend ? __builtin_amdgcn_exp2f(m - m_pend) : 1.0f;
+      m = pend ? m_pend : m;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) o[d] = o[d] * alpha;
+      pend = false;
+    }
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[kt][u][j] = (_Float16)__builtin_amdgcn_exp2f(sc[kt][8 * u + j]);
+    float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
+    float my = max3f(sc[1][0], sc[1][1], sc[1][2]);
+#pragma unroll
+    for (int r = 3; r + 1 < 16; r += 2) {
+      mx = max3f(mx, sc[0][r], sc[0][r + 1]);
+      my = max3f(my, sc[1][r], sc[1][r + 1]);
+    }
+    mx = max3f(mx, my, fmaxf(sc[0][15], sc[1][15]));
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(int, mx), __builtin_bit_cast(int, mx),
+                                                       false, false);
+      mx = fmaxf(__builtin_bit_cast(float, (int)sw[0]), __builtin_bit_cast(float, (int)sw[1]));
+    }
+    const float mrow = mx + moff;
+    const bool unsafe = !(mrow <= m + 15.0f);   // (m = -inf: unsafe)
+    if (__any(unsafe)) {
+      const float mnew = unsafe ? mrow : m;
+      const float alpha = unsafe ? __builtin_amdgcn_exp2f(m - mnew) : 1.0f;
+      m = mnew;
+#pragma unroll
+      for (int d = 0; d < 3; ++d) o[d] = o[d] * alpha;
+      const float delta = m - moff;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pb[kt][u][j] = (_Float16)__builtin_amdgcn_exp2f(sc[kt][8 * u + j] - delta);
+    }
+    pend = mrow > m + 8.0f;
+    m_pend = mrow;
+    if (kh + 1 < S) {
+      th_cur = (float)thw[(kh + 1) * 32 + l32];
+      moff = pend ? m_pend : m;
+      coff = th_cur - moff;
+    }
+  };
   auto softmax = [&](int kh) {
+    if constexpr (COFF) return softmax_coff(kh);
     if (__any(pend)) {   // last row's deferred offset move
       const float alpha = pend ? __builtin_amdgcn_exp2f(m - m_pend) : 1.0f;
       m = pend ? m_pend : m;
@@ -1215,6 +1278,8 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     case 2: hipLaunchKernelGGL(glob80_attention_kernel<2>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 8: hipLaunchKernelGGL(glob80_attention_kernel<8>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 9: hipLaunchKernelGGL(glob80_attention_kernel<9>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     default: hipLaunchKernelGGL(glob80_attention_kernel<0>, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
   }
 #else

@@ -968,7 +968,8 @@ void w4a16_gemm_v4(const _Float16* __restrict__ A, int64_t lda, const u32x4* __r
 
 // y = acc * s[n] + b[n] (-> GELU / residual add), staged through LDS in EP_ROWS-row slices per
 // wave so the global traffic is row-contiguous 16-byte vectors (v3's epilogue)
-template <int TM, int TN, int EP_ROWS, int EPI>
+// EVAR (tuning build, timing-only): 1 = f16 outputs staged but not stored, 2 = no scale / bias / GELU
+template <int TM, int TN, int EP_ROWS, int EPI, int EVAR = 0>
 __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], const float (&csc)[TN],
                                             const float (&cb)[TN], char* ep_bytes, void* Cout, int64_t ldc,
                                             int M, int row_base, int col_base, int lane,
@@ -1030,9 +1031,10 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
         const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel - sl * EP_ROWS;   // row within the slice (r + 1: rl + 1)
 #pragma unroll
         for (int t = 0; t < TN; ++t) {
-          float2_t v = __builtin_elementwise_fma((float2_t){acc[i][t][r], acc[i][t][r + 1]}, (float2_t)(csc[t]),
-                                                 (float2_t)(lnf_consumer(EPI) ? 0.0f : cb[t]));
-          if (EPI == SAMQ_EPI_BIAS_GELU) v = gelu_fast2(v);
+          float2_t v = (EVAR & 2) ? (float2_t){acc[i][t][r], acc[i][t][r + 1]}
+                                  : __builtin_elementwise_fma((float2_t){acc[i][t][r], acc[i][t][r + 1]}, (float2_t)(csc[t]),
+                                                              (float2_t)(lnf_consumer(EPI) ? 0.0f : cb[t]));
+          if (EPI == SAMQ_EPI_BIAS_GELU && !(EVAR & 2)) v = gelu_fast2(v);
           ep[rl * WN + t * 32 + (lane & 31)] = v.x;
           ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
         }
@@ -1085,7 +1087,7 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
             if (row < M) {
               const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
                                  (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
-              *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
+              if (!(EVAR & 1) || (float)h[0] == 1234.5f) *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) = h;
             }
           }
         }
@@ -1225,11 +1227,11 @@ __device__ __forceinline__ void vm_wait_le(int n) {   // s_waitcnt vmcnt(n) for 
 }
 
 template <int WAVES_M, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
-__global__ __launch_bounds__(512, 1)
-void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
+__device__ __forceinline__
+void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
                     const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
                     const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
-                    int M, int N, int K, int kpg, LnfArgs lnf) {
+                    int M, int N, int K, int kpg, LnfArgs lnf, int bid) {
   constexpr int NW = 8;
   constexpr int WAVES_N = NW / WAVES_M;
   constexpr int WM = TM * 32, WN = TN * 32;
@@ -1305,7 +1307,7 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
   int m0, n0;
-  xcd_tile(blockIdx.x, tiles_m, tiles_n, (VAR & 64) != 0, m0, n0);
+  xcd_tile(bid, tiles_m, tiles_n, (VAR & 64) != 0, m0, n0);
   m0 *= BM;
   n0 *= BN;
   const int kt_count = K / BK;
@@ -1438,6 +1440,21 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
       }
   }
 
+  // VAR & (1 << 21): the epilogue's per-channel scale / bias of this lane's columns loaded before
+  // the prologue's LDS-DMA pieces (the prologue's retire wait covers them) and kept in VGPRs over
+  // the main loop, instead of loaded after it, where their latency sits behind the epilogue barrier
+  constexpr bool EARLY_EP = (VAR & (1 << 21)) != 0;
+  static_assert(!EARLY_EP || !(GR || TE || lnf_consumer(EPI) || lnf_producer(EPI)), "early epilogue operands");
+  constexpr int NEC = EARLY_EP ? (M16 ? 2 * TN : TN) : 1;
+  _Float16 esc[NEC], ebi[NEC];
+  if constexpr (EARLY_EP) {
+#pragma unroll
+    for (int e = 0; e < NEC; ++e) {
+      const int c = M16 ? n0 + wn * WN + 32 * (e >> 1) + 16 * (e & 1) + (lane & 15) : col[e];
+      esc[e] = scales[c];
+      ebi[e] = bias ? bias[c] : (_Float16)0.0f;
+    }
+  }
   // VAR & 256: static priority instead of per-segment flips -- the second-dispatched half (group 1,
   // the arbitration loser) at prio 1 for the whole loop (MI355X_MICROARCH.md two-waves item 4)
   if ((VAR & 256) && grp) __builtin_amdgcn_s_setprio(1);
@@ -1698,8 +1715,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int c = n0 + wn * WN + 32 * t + 16 * h + ql;
-        csc16[t][h] = GR ? 1.0f : (float)scales[c];
-        cb16[t][h] = bias ? (float)bias[c] : 0.0f;
+        csc16[t][h] = EARLY_EP ? (float)esc[EARLY_EP ? 2 * t + h : 0] : GR ? 1.0f : (float)scales[c];
+        cb16[t][h] = EARLY_EP ? (float)ebi[EARLY_EP ? 2 * t + h : 0] : bias ? (float)bias[c] : 0.0f;
       }
     __syncthreads();
     float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES) + wm * WM;
@@ -1714,8 +1731,8 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   float csc[TN], cb[TN];
 #pragma unroll
   for (int t = 0; t < TN; ++t) {
-    csc[t] = GR ? 1.0f : (float)scales[col[t]];
-    cb[t] = bias ? (float)bias[col[t]] : 0.0f;
+    csc[t] = EARLY_EP ? (float)esc[EARLY_EP ? t : 0] : GR ? 1.0f : (float)scales[col[t]];
+    cb[t] = EARLY_EP ? (float)ebi[EARLY_EP ? t : 0] : bias ? (float)bias[col[t]] : 0.0f;
   }
   __syncthreads();
   float2_t* rowinfo = (float2_t*)(smem + NW * EP_BYTES) + wm * WM;
@@ -1723,8 +1740,33 @@ void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __
   if constexpr (lnf_consumer(EPI))
     lnf_rowinfo_wg<BM, NW>(lnf, (float2_t*)(smem + NW * EP_BYTES), smem + NW * EP_BYTES + RI_BYTES, M, m0, n0 == 0,
                            wave, lane);
-  pp_epilogue<TM, TN, EP_ROWS, EPI>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
-                                    n0 + wn * WN, lane, lnf, N, rowinfo);
+  pp_epilogue<TM, TN, EP_ROWS, EPI, (VAR >> 17) & 3>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
+                                                     n0 + wn * WN, lane, lnf, N, rowinfo);
+}
+
+// The ping-pong GEMM kernel: one tile per workgroup, or (VAR & (1 << 20), persistent) a grid of at
+// most one workgroup per CU looping over the tiles t = blockIdx.x, + gridDim.x, ... -- the tile's
+// epilogue stores drain while the next tile's prologue DMA and first K tiles run (a one-tile
+// workgroup holds its CU until its stores are acknowledged).  gridDim.x % 8 == 0 keeps every tile
+// on the XCD its one-tile launch would give it (xcd_tile's t % 8 map).
+template <int WAVES_M, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
+__global__ __launch_bounds__(512, 1)
+void w4a16_gemm_pp2(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restrict__ Wp,
+                    const _Float16* __restrict__ scales, const uint32_t* __restrict__ qzeros,
+                    const _Float16* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
+                    int M, int N, int K, int kpg, LnfArgs lnf) {
+  if constexpr ((VAR & (1 << 20)) != 0) {
+    constexpr int BM = WAVES_M * TM * 32, BN = (8 / WAVES_M) * TN * 32;
+    const int ntiles = ((M + BM - 1) / BM) * (N / BN);
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+      pp2_tile<WAVES_M, TM, TN, NPH, STAGES, LA, EPI, VAR>(A, lda, Wp, scales, qzeros, bias, Cout, ldc, M, N, K, kpg,
+                                                           lnf, t);
+      __syncthreads();   // the epilogue's LDS reads before the next tile's ring DMA
+    }
+  } else {
+    pp2_tile<WAVES_M, TM, TN, NPH, STAGES, LA, EPI, VAR>(A, lda, Wp, scales, qzeros, bias, Cout, ldc, M, N, K, kpg, lnf,
+                                                         blockIdx.x);
+  }
 }
 
 // ------------------------------------------------------------------ dispatch
@@ -1761,6 +1803,16 @@ static int launch_v4(const GemmArgs& a, hipStream_t st) {
   return SAMQ_OK;
 }
 
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 template <int WMW, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
 static int launch_pp2(const GemmArgs& a, hipStream_t st) {
   constexpr int BM = WMW * TM * 32, BN = (8 / WMW) * TN * 32;
@@ -1770,7 +1822,8 @@ static int launch_pp2(const GemmArgs& a, hipStream_t st) {
     constexpr int kmax = Pp2Lds<WMW, TM, TN, STAGES, EPI, VAR>::LNF_KMAX;
     if (a.K > kmax) return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm_lnf: consumer K exceeds this config's LDS row-partial budget");
   }
-  const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
+  if ((VAR & (1 << 20)) != 0 && nwg > cu_count()) nwg = cu_count() & ~7;   // persistent: <= 1 workgroup per CU
   hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
                      a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64, a.lnf);
   SAMQ_LAUNCH_CHECK("w4a16_gemm_pp2 launch");
@@ -1820,6 +1873,13 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
       // cfg 57 / 64 with the LDS-DMA pieces spread through the MFMA burst (VAR & 16384)
       case 100: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 16384>(a, st);
+      // cfg 57 / 64 persistent (one workgroup per CU loops over the tiles: stores drain under the
+      // next tile's prologue)
+      case 107: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 20)>(a, st);
+      // cfg 57 / 64 with the epilogue's scale / bias loaded before the prologue (VAR & (1 << 21))
+      case 109: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 21)>(a, st);
+      case 110: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | (1 << 21)>(a, st);
+      case 108: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | (1 << 20)>(a, st);
       // cfg 57 with transposed accumulators and the f16-staged epilogue (f16 outputs only)
       case 104:
         if constexpr (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 65536>(a, st);
@@ -1870,6 +1930,9 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 98: return launch_pp2<1, 4, 2, 2, 5, 4, EPI, 4096>(a, st);
       // timing-only: cfg 57 / 64 without the epilogue (the per-tile epilogue cost)
       case 102: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 32768>(a, st);
+      // timing-only: cfg 57 whose f16 epilogue stages but does not store (105) / skips the math (106)
+      case 105: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 17)>(a, st);
+      case 106: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (2 << 17)>(a, st);
       case 103: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 32768>(a, st);
       case 71: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 2>(a, st);   // timing-only: cfg 57 without MFMA
       case 72: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 3>(a, st);   // timing-only: neither
@@ -1966,7 +2029,7 @@ static int cfg_bn(int cfg) {
                  case 74: case 75: case 76: case 77: case 78: case 79: return 256;
                  case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
                  case 97: case 98: return 512;
-                 case 100: case 101: case 102: case 103: case 104: return 256;
+                 case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109: case 110: return 256;
                  default: return 0; }
 }
 

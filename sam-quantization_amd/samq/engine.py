@@ -59,6 +59,9 @@ class EncoderEngine:
         # (x += y in f32); "ln32" = the GEMM stores y (f32) and the next LayerNorm adds it
         # (samq_add_layernorm, bit-identical x); "ln16" = the same with y stored as f16
         self.res_mode = "epi"
+        # timing-only A/B knob (tools): launches to leave out of the W4A16 block ("ln", "win",
+        # "glob") -- the output is wrong; the empty default runs everything
+        self.skip = frozenset()
         self.plans = []
         for blk in enc.blocks:
             attn = blk.attn
@@ -312,18 +315,21 @@ class EncoderEngine:
         x, xn, qkv, att, hid = bufs["x"], bufs["xn"], bufs["qkv"], bufs["att"], bufs["hid"]
         late = self.res_mode != "epi"
         res_epi = ops.EPI_BIAS if self.res_mode == "ln16" else ops.EPI_F32
-        self._res_add_ln(x, bufs, p.ln1_w, p.ln1_b, p.ln1_eps, xn, late and not first)
+        if "ln" not in self.skip:
+            self._res_add_ln(x, bufs, p.ln1_w, p.ln1_b, p.ln1_eps, xn, late and not first)
         mark(0)
         p.qkv.forward_epilogue(xn, ops.EPI_BIAS, out=qkv)
         mark(1)
-        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
+        if ("win" if p.window else "glob") not in self.skip:
+            ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att)
         mark(2)
         if late:
             p.proj.forward_epilogue(att, res_epi, out=self._delta(bufs))
         else:
             p.proj.forward_epilogue(att, ops.EPI_RESADD_F32, out=x)
         mark(3)
-        self._res_add_ln(x, bufs, p.ln2_w, p.ln2_b, p.ln2_eps, xn, late)
+        if "ln" not in self.skip:
+            self._res_add_ln(x, bufs, p.ln2_w, p.ln2_b, p.ln2_eps, xn, late)
         mark(4)
         p.lin1.forward_epilogue(xn, ops.EPI_BIAS_GELU, out=hid)
         mark(5)

@@ -98,7 +98,7 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
         _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
 
 
-@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101, 104])
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101, 104, 107, 108, 109, 110])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
@@ -113,6 +113,32 @@ def test_w4a16_gemm_pingpong(cuda, cfg, epi):
         a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
         y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
         _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, -1, epi, cfg, rng)
+
+
+@pytest.mark.parametrize("cfg,base", [(107, 57), (108, 64)])
+@pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
+def test_w4a16_gemm_persistent_matches(cuda, cfg, base, epi):
+    """The persistent ping-pong form (one workgroup per CU looping over the tiles) computes every
+    tile exactly like its one-tile-per-workgroup twin: bit-identical at M = 16384, N = 1280
+    (320 tiles on <= 256 workgroups, so workgroups run two tiles) and at a ragged M."""
+    from samq import ops
+    for m, k, n in ((16384, 1280, 1280), (9000, 640, 768)):
+        qw, qz, sc, bias = _packed_layer(k, n, -1, seed=cfg + k)
+        g = torch.Generator(device=cuda).manual_seed(m)
+        a = torch.randn((m, k), generator=g, device=cuda).half()
+        packed = ops.w4_repack(_dev(qw, cuda))
+        args = (a, packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, -1)
+        e = {"bias": ops.EPI_BIAS, "gelu": ops.EPI_BIAS_GELU, "resadd": ops.EPI_RESADD_F32, "f32": ops.EPI_F32}[epi]
+        if e == ops.EPI_RESADD_F32:
+            r0 = torch.randn((m, n), generator=g, device=cuda)
+            o1, o2 = r0.clone(), r0.clone()
+            ops.w4a16_gemm(*args, e, out=o1, cfg=base)
+            ops.w4a16_gemm(*args, e, out=o2, cfg=cfg)
+        else:
+            o1 = ops.w4a16_gemm(*args, e, cfg=base)
+            o2 = ops.w4a16_gemm(*args, e, cfg=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(o1, o2), (m, k, n)
 
 
 @pytest.mark.parametrize("cfg", [57, 64])

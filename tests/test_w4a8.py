@@ -203,10 +203,12 @@ def _float_close(out, ref, rtol, atol_frac, what):
 # off-by-one budgets: the integer-exact stages (LN-q, lin1 + GELU-q) may only differ from the
 # oracle's fp32 graph at rounding ties of its own fp32 sums; the attention store quantises an
 # fp16-arithmetic attention (fp16 Q/K/V/P on the MFMA, fp32 softmax) against the oracle's fp32
-# attention, measured (ViT-H, 1024^2, round 3) at 3.7e-3 (window) / 5.3e-3 (global) of codes --
-# bound 8e-3; the integer-exact stages measured 1e-6 .. 4e-6
+# attention.  Measured (ViT-H, 1024^2): round 3, quantising the fp16-rounded output, 3.7e-3
+# (window) / 5.3e-3 (global); round 4, quantising the f32 output (attn_store4), 2.7-3.0e-3 (window)
+# / 0.93-0.98e-3 (global), per-channel and G = 128 -- bound 5e-3; the integer-exact stages
+# measured 0 .. 4e-6
 W4A8_EXACT_FRAC = 1e-4
-W4A8_ATTN_FRAC = 8e-3
+W4A8_ATTN_FRAC = 5e-3
 
 
 @pytest.mark.gpu

@@ -32,6 +32,7 @@ graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.ln_rpw = cfg.get("ln_rpw", 0)
     eng.res_mode = cfg.get("res", "epi")   # where the proj / lin2 residual adds run (engine.res_mode)
+    eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only: "skip_ln=1" etc.
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).gemm_cfg = cfg.get(lay, 0)
