@@ -29,7 +29,10 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <string>
 #include <type_traits>
+#include <vector>
 
 namespace samq {
 
@@ -61,10 +64,10 @@ struct AttnParams {
 // flips).
 __device__ __forceinline__ void attn_store4(const AttnParams& p, int64_t off, float4_t o) {
   if (p.out_scale > 0.f) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)q8_exact(o[e], p.out_scale, p.out_inv) & 0xFFu) << (8 * e);
-    *(uint32_t*)((int8_t*)p.out + off) = w;
+    const float lim = 130.0f * p.out_scale;
+    const float2_t c01 = q8_exact2(float2_t{o[0], o[1]}, p.out_scale, p.out_inv, lim);
+    const float2_t c23 = q8_exact2(float2_t{o[2], o[3]}, p.out_scale, p.out_inv, lim);
+    *(uint32_t*)((int8_t*)p.out + off) = q8_pack4(c01.x, c01.y, c23.x, c23.y);
   } else {
     *(half4_t*)(p.out + off) = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
   }
@@ -523,7 +526,12 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
 //    window's keys in the exp2 domain, O^T += V^T.P^T two key rows per MFMA with P^T in the score
 //    registers' own k order, the row sum as one more MFMA against ones.
 // pieces of the window kernel
-template <int D>
+// UNSC (round 4): Q enters the MFMAs unscaled (exact fp16 qkv values) and the scores stay in
+// unscaled units S_u = q.k + (q.Rw + fp16(q.Rh)) / scale, the sm scale and log2e applied inside the
+// softmax's exp2 argument (one fma per score, as the subtraction it replaces): no fp16 rounding of
+// q * scale * log2e (a 2^-12 relative error on every score), and TH rounded to fp16 where the
+// reference rounds rel_h (q . Rh, unscaled)
+template <int D, bool UNSC = false>
 struct Win {
   static constexpr int S = 14, QT = 2;
   static constexpr int KS = D == 80 ? 3 : 2;            // k32 steps of Q.K^T
@@ -640,7 +648,7 @@ struct Win {
         relw[t][s] = *(const half8_t*)(tabh + TAB + idx * D + dd);
       }
     }
-    // ---- Q scale (fp16(q * scale * log2e), the reference's rounding) and rel-pos terms
+    // ---- Q scale (fp16(q * scale * log2e), the reference's rounding; UNSC: unscaled) and rel-pos terms
     half8_t qf[QT][KS];
     float4_t tw[QT];
     half8_t th[QT][2];
@@ -649,8 +657,10 @@ struct Win {
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         half8_t v = qraw[t][s];
+        if constexpr (!UNSC) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (_Float16)__builtin_fmaf((float)v[j], qscale, 0.0f);
+          for (int j = 0; j < 8; ++j) v[j] = (_Float16)__builtin_fmaf((float)v[j], qscale, 0.0f);
+        }
         qf[t][s] = v;
       }
       float4_t a = {0.f, 0.f, 0.f, 0.f}, c = {0.f, 0.f, 0.f, 0.f};
@@ -659,8 +669,8 @@ struct Win {
         a = __builtin_amdgcn_mfma_f32_16x16x32_f16(relw[t][s], qf[t][s], a, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(relh[t][s], qf[t][s], c, 0, 0, 0);
       }
-      a = a * inv_scale;
-      c = c * inv_scale;
+      a = a * inv_scale;                 // UNSC: (q . Rw) / scale; else log2e q . Rw
+      if constexpr (!UNSC) c = c * inv_scale;   // UNSC: q . Rh, rounded below like rel_h
       if (g == 3) { a[2] = -INFINITY; a[3] = -INFINITY; }   // key slots 14, 15
       tw[t] = a;
       // lane (g, ql) holds TH[kh = 4g..4g+3][query ql]; gather kh 0..15 of its query from the
@@ -689,7 +699,7 @@ struct Win {
       }
 #pragma unroll
       for (int t = 0; t < QT; ++t) {
-        const float h = (float)th[t][kh >> 3][kh & 7];
+        const float h = UNSC ? (float)th[t][kh >> 3][kh & 7] * inv_scale : (float)th[t][kh >> 3][kh & 7];
         float4_t a = tw[t] + h;
 #pragma unroll
         for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kh & 1][s], qf[t][s], a, 0, 0, 0);
@@ -716,13 +726,24 @@ struct Win {
       }
       mx = fmaxf(mx, my);
       mx = max_rows4(mx);
+      if constexpr (UNSC) {   // P = exp2((S_u - max) * scale * log2e) as one fma per score
+        const float nmx = -mx * qscale;
 #pragma unroll
-      for (int pr = 0; pr < S / 2; ++pr)
+        for (int pr = 0; pr < S / 2; ++pr)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pb[t][pr][r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr][r] - mx);
-          pb[t][pr][4 + r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr + 1][r] - mx);
-        }
+          for (int r = 0; r < 4; ++r) {
+            pb[t][pr][r] = (_Float16)__builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][2 * pr][r], qscale, nmx));
+            pb[t][pr][4 + r] = (_Float16)__builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][2 * pr + 1][r], qscale, nmx));
+          }
+      } else {
+#pragma unroll
+        for (int pr = 0; pr < S / 2; ++pr)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pb[t][pr][r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr][r] - mx);
+            pb[t][pr][4 + r] = (_Float16)__builtin_amdgcn_exp2f(sc[t][2 * pr + 1][r] - mx);
+          }
+      }
     }
 
     // ---- O^T = V^T . P^T (two key rows per MFMA), l = ones . P^T
@@ -797,9 +818,9 @@ struct Win {
 // One item per 4-wave workgroup, two workgroups per CU (rows 2w, 2w+1 then 8+2w, 9+2w).  (A
 // persistent form -- one 8-wave workgroup per CU, wave 7 streaming the next item's K/V into a second
 // buffer while waves 0..6 compute -- measured 37.9 vs 37.0 us per 2-image ViT-H launch.)
-template <int D>
+template <int D, bool UNSC = false>
 __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int items) {
-  using W = Win<D>;
+  using W = Win<D, UNSC>;
   static_assert(W::KVB + W::TABB <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) char smem[W::KVB + W::TABB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -854,11 +875,20 @@ __device__ __forceinline__ float16_t mfma32(half8_t a, half8_t b, float16_t c) {
 
 #ifdef SAMQ_TUNING
 __device__ unsigned long long g_attn_stamps[8];   // timing experiments (tuning build)
+__device__ unsigned long long g_attn_wgt[4096 * 6];   // DBG & 8: per-workgroup timeline
 #endif
+template <int DBG>
+__device__ __forceinline__ void wg_mark(unsigned long long (&t)[6], int k) {
+  if constexpr ((DBG & 8) != 0) {
+    t[k] = __builtin_amdgcn_s_memrealtime();
+    if (k == 1 || k == 2) t[k + 3] = __builtin_amdgcn_s_memtime();
+  }
+}
 
 // DBG (tuning build only): & 1 per-wave s_memtime stamps of the four loop segments; & 2 no exp2,
-// & 4 no MFMAs (timing-only variants, wrong results); & 8 the softmax offset folded into the
-// Q.K^T C input (COFF below)
+// & 4 no MFMAs (timing-only variants, wrong results); & 8 per-workgroup timeline (realtime at
+// entry / loop start / loop end / exit + shader clock over the loop); & 16 the round-3 softmax (offset subtracted
+// in the softmax segment instead of folded into the Q.K^T C input, COFF below)
 template <int DBG>
 __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) {
   constexpr int D = 80, S = 64, KS = 5;
@@ -868,12 +898,19 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   constexpr int THB = 64 * 32 * 2;                // per wave: fp16 TH[kh][q]
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 8 * THB];
   constexpr bool DBG_NOEXP = (DBG & 2) != 0, DBG_NOMFMA = (DBG & 4) != 0;
-  // COFF: the next row's TH and softmax offset enter its Q.K^T as part of the C input
+  // COFF (round 4): the next row's TH and softmax offset enter its Q.K^T as part of the C input
   // (C = TW + (TH[kh] - offset), a per-lane scalar added in the MFMA segment), so the softmax
-  // segment -- the longer of the two -- runs exp2 straight on the scores (32 fewer v_sub per row)
-  constexpr bool COFF = (DBG & 8) != 0;
+  // segment -- the longer of the two -- runs exp2 straight on the scores (32 fewer v_sub per row):
+  // 204.1 vs 209.6 us per 2-image launch, outputs within 3e-5 (profiles/r4_i.attn.log)
+  constexpr bool COFF = (DBG & 16) == 0;
+  // round 4 loop variants (tuning A/B): & 32 the next row's K fragment reads issued at the start of
+  // the VALU segment; & 64 the first P.V step's V^T fragments read at the end of the VALU segment;
+  // & 128 without PFENCE
+  constexpr bool KEARLY = (DBG & 32) != 0, VPRE = (DBG & 64) != 0, PFENCE = (DBG & 128) == 0;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
+  unsigned long long wgt[6] = {0, 0, 0, 0, 0, 0};
+  wg_mark<DBG>(wgt, 0);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1031,6 +1068,9 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) pb[kt][u][j] = (_Float16)__builtin_amdgcn_exp2f(sc[kt][8 * u + j]);
+    // PFENCE: keep the fast-path exp2s ahead of the max chain (the compiler otherwise sinks them
+    // into the not-unsafe branch, behind the serial max3 / permlane / compare chain)
+    if constexpr (PFENCE) asm volatile("" : "+v"(pb[0][0]), "+v"(pb[0][1]), "+v"(pb[1][0]), "+v"(pb[1][1]));
     float mx = max3f(sc[0][0], sc[0][1], sc[0][2]);
     float my = max3f(sc[1][0], sc[1][1], sc[1][2]);
 #pragma unroll
@@ -1130,10 +1170,19 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     lo[2] = ds_read_tr16_off<KQ * 640>(vb2 + rb);
     hi[2] = ds_read_tr16_off<(KQ + 2) * 640>(vb2 + rb);
   };
+  half4_t vlo0[3], vhi0[3];   // VPRE: the t = 0 fragments, read in the VALU segment
   auto pv = [&](int slot) {   // O^T += V^T . P^T: 4 k16-steps x 3 d-blocks, next step's reads in flight
     const uint32_t rb = slot * ROWB;
     half4_t lo[2][3], hi[2][3];
-    vread(std::integral_constant<int, 0>{}, rb, lo[0], hi[0]);
+    if constexpr (VPRE) {
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        lo[0][d] = vlo0[d];
+        hi[0][d] = vhi0[d];
+      }
+    } else {
+      vread(std::integral_constant<int, 0>{}, rb, lo[0], hi[0]);
+    }
     static_for<4>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       constexpr int cb = t & 1;
@@ -1181,18 +1230,12 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   //    segment of row r-2, group 1 at the end of its VALU segment of row r-2.
   // The asm fences pin the softmax results and K fragments to their segment (the compiler would
   // otherwise sink the exp2s past the barrier into the MFMA segment).
-  auto retire = [&](int newer) {   // s_waitcnt vmcnt(newer) for a wave-uniform newer in {0, 2, 3, 4, 6}
-    if (newer >= 6) wait_vmcnt<6>();
-    else if (newer >= 4) wait_vmcnt<4>();
-    else if (newer >= 3) wait_vmcnt<3>();
-    else if (newer >= 2) wait_vmcnt<2>();
-    else wait_vmcnt<0>();
-  };
   wait_vmcnt<0>();
   __syncthreads();   // rows 0..3 landed; TH visible
   kread(smem);
   qk();
   if (grp) __builtin_amdgcn_s_barrier();
+  wg_mark<DBG>(wgt, 1);
   unsigned long long ph[4] = {0, 0, 0, 0}, tprev = 0;
   auto stamp = [&](int k) {
     if constexpr ((DBG & 1) != 0) {
@@ -1213,14 +1256,30 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     asm volatile("" : "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]), "+v"(kf[1][4]),
                  "+v"(o[0]), "+v"(o[1]), "+v"(o[2]) :: "memory");
   };
+  // ring slots as rotating wave-uniform counters (no per-row modulo); constant vmcnt counts per
+  // group: group 0 (waves 0..3) issues 3 pieces per row, group 1 two
+  static_assert(NI == 3, "vmcnt counts below: 3 / 2 pieces per row for group 0 / 1");
+  int j = 0;   // kh % NSLOT
   for (int kh = 0; kh < S; ++kh) {
+    const int j1 = j == NSLOT - 1 ? 0 : j + 1, j4 = j == 0 ? NSLOT - 1 : j - 1;
     stamp(3);
     fence_sc();
+    if constexpr (KEARLY) {
+      if (kh + 1 < S) kread(smem + j1 * ROWB);
+    }
     softmax(kh);
-    if (kh + 1 < S) kread(smem + ((kh + 1) % NSLOT) * ROWB);
+    if constexpr (!KEARLY) {
+      if (kh + 1 < S) kread(smem + j1 * ROWB);
+    }
+    if constexpr (VPRE) vread(std::integral_constant<int, 0>{}, j * ROWB, vlo0, vhi0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     fence_pk();
-    if (grp && kh + 2 < S) retire(kh + 3 < S ? npc : 0);   // row kh+2 (rows kh+3 newer)
+    if constexpr (VPRE)
+      asm volatile("" : "+v"(vlo0[0]), "+v"(vlo0[1]), "+v"(vlo0[2]), "+v"(vhi0[0]), "+v"(vhi0[1]), "+v"(vhi0[2]));
+    if (grp && kh + 2 < S) {   // row kh+2 (row kh+3 newer)
+      if (kh + 3 < S) wait_vmcnt<2>();
+      else wait_vmcnt<0>();
+    }
     stamp(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -1228,16 +1287,21 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     stamp(1);
     fence_pk();
     __builtin_amdgcn_s_setprio(1);
-    if (kh + 4 < S) issue(kh + 4, (kh + 4) % NSLOT);
-    pv(kh % NSLOT);
+    if (kh + 4 < S) issue(kh + 4, j4);
+    pv(j);
     if (kh + 1 < S) qk();
     fence_sc();
     __builtin_amdgcn_s_setprio(0);
-    if (!grp && kh + 2 < S) retire(npc * ((kh + 3 < S ? 1 : 0) + (kh + 4 < S ? 1 : 0)));   // row kh+2
+    if (!grp && kh + 2 < S) {   // row kh+2 (rows kh+3, kh+4 newer)
+      if (kh + 4 < S) wait_vmcnt<6>();
+      else if (kh + 3 < S) wait_vmcnt<3>();
+      else wait_vmcnt<0>();
+    }
     stamp(2);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    j = j1;
   }
 #ifdef SAMQ_TUNING
   if ((DBG & 1) && lane == 0) {
@@ -1246,6 +1310,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   }
 #endif
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
+  wg_mark<DBG>(wgt, 2);
 
   // ---- normalise + store: lane = query (qh, qw0 + l32), dims 32 db + 8 c + 4 h .. + 3
   const float inv = 1.0f / o[2][8];
@@ -1258,6 +1323,15 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       const float4_t v = {o[db][4 * c], o[db][4 * c + 1], o[db][4 * c + 2], o[db][4 * c + 3]};
       attn_store4(p, dst_tok + 32 * db + 8 * c + 4 * h, v * inv);
     }
+#ifdef SAMQ_TUNING
+  if constexpr ((DBG & 8) != 0) {
+    wg_mark<DBG>(wgt, 3);
+    if (tid == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) g_attn_wgt[blockIdx.x * 6 + k] = wgt[k];
+    }
+  }
+#endif
 }
 
 static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
@@ -1279,7 +1353,14 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 8: hipLaunchKernelGGL(glob80_attention_kernel<8>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
-    case 9: hipLaunchKernelGGL(glob80_attention_kernel<9>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 32: hipLaunchKernelGGL(glob80_attention_kernel<32>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 64: hipLaunchKernelGGL(glob80_attention_kernel<64>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 96: hipLaunchKernelGGL(glob80_attention_kernel<96>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 128: hipLaunchKernelGGL(glob80_attention_kernel<128>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 160: hipLaunchKernelGGL(glob80_attention_kernel<160>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 224: hipLaunchKernelGGL(glob80_attention_kernel<224>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 16: hipLaunchKernelGGL(glob80_attention_kernel<16>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 17: hipLaunchKernelGGL(glob80_attention_kernel<17>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     default: hipLaunchKernelGGL(glob80_attention_kernel<0>, dim3(16 * p.heads * units), dim3(512), 0, stream, q);
   }
 #else
@@ -1296,6 +1377,31 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
             "%.0f M %.0f bar %.0f\n", hst[0] / n, hst[1] / n, hst[2] / n, hst[3] / n, hst[4] / n, hst[5] / n,
             hst[6] / n, hst[7] / n);
   }
+  if (q.dbg & 8) {   // per-workgroup timeline (realtime ticks = 10 ns)
+    const int nwg = 16 * p.heads * units;
+    std::vector<unsigned long long> t((size_t)nwg * 6);
+    (void)hipStreamSynchronize(stream);
+    (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_attn_wgt), t.size() * 8);
+    unsigned long long t0 = ~0ull, t3 = 0;
+    for (int i = 0; i < nwg; ++i) { t0 = std::min(t0, t[i * 6]); t3 = std::max(t3, t[i * 6 + 3]); }
+    std::vector<double> st, pro, lp, epi, clk, fin;
+    for (int i = 0; i < nwg; ++i) {
+      const unsigned long long* w = &t[i * 6];
+      st.push_back((w[0] - t0) * 0.01); pro.push_back((w[1] - w[0]) * 0.01); lp.push_back((w[2] - w[1]) * 0.01);
+      epi.push_back((w[3] - w[2]) * 0.01); fin.push_back((w[3] - t0) * 0.01);
+      clk.push_back(w[2] > w[1] ? (double)(w[5] - w[4]) / ((w[2] - w[1]) * 10.0) : 0.0);
+    }
+    auto q5 = [](std::vector<double> v) {
+      std::sort(v.begin(), v.end());
+      const size_t n = v.size();
+      char b[160];
+      snprintf(b, sizeof(b), "min %.2f p25 %.2f med %.2f p75 %.2f max %.2f", v[0], v[n / 4], v[n / 2], v[3 * n / 4], v[n - 1]);
+      return std::string(b);
+    };
+    fprintf(stderr, "glob80 timeline: span %.2f us over %d workgroups\n  start(us) %s\n  prologue(us) %s\n  loop(us) %s\n"
+            "  epilogue(us) %s\n  finish(us) %s\n  loop clock(GHz) %s\n", (t3 - t0) * 0.01, nwg, q5(st).c_str(),
+            q5(pro).c_str(), q5(lp).c_str(), q5(epi).c_str(), q5(fin).c_str(), q5(clk).c_str());
+  }
 #endif
   return SAMQ_OK;
 }
@@ -1303,6 +1409,14 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
 template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
+#ifdef SAMQ_TUNING
+  const char* e = getenv("SAMQ_ATTN_WIN");   // tuning A/B: 1 = the unscaled-Q variant (Win UNSC)
+  if (e && atoi(e) == 1) {
+    hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
+    SAMQ_LAUNCH_CHECK("win_attention launch");
+    return SAMQ_OK;
+  }
+#endif
   hipLaunchKernelGGL((win_attention_kernel<D>), dim3(items), dim3(256), 0, stream, p, items);
   SAMQ_LAUNCH_CHECK("win_attention launch");
   return SAMQ_OK;

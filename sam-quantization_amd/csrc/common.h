@@ -102,6 +102,29 @@ __device__ __forceinline__ float q8_exact(float v, float s, float inv) {
   return fminf(fmaxf(r, -128.f), 127.f);
 }
 
+// q8_exact on a packed pair (v_pk_mul / v_pk_fma: the same IEEE operations, so each half is
+// bit-identical to q8_exact), with |v| first clamped to lim (>= 128.5 s: every larger |v| gives the
+// same saturated code, and the quotients stay finite -- no isfinite select) and the code clamp on
+// v_med3.  Returns the codes as floats in [-128, 127].
+__device__ __forceinline__ float2_t q8_exact2(float2_t v, float s, float inv, float lim) {
+  v = float2_t{__builtin_amdgcn_fmed3f(v.x, -lim, lim), __builtin_amdgcn_fmed3f(v.y, -lim, lim)};
+  const float2_t sv = (float2_t)(s), iv = (float2_t)(inv);
+  const float2_t q = v * iv;
+  const float2_t q1 = __builtin_elementwise_fma(__builtin_elementwise_fma(-q, sv, v), iv, q);
+  const float2_t q2 = __builtin_elementwise_fma(__builtin_elementwise_fma(-q1, sv, v), iv, q1);
+  return float2_t{__builtin_amdgcn_fmed3f(__builtin_rintf(q2.x), -128.f, 127.f),
+                  __builtin_amdgcn_fmed3f(__builtin_rintf(q2.y), -128.f, 127.f)};
+}
+// four codes (integer floats in [-128, 127]) -> their int8 bytes in one dword: v_cvt_pk_u8_f32 of
+// code + 128 (exact integers in [0, 255]) per byte, then the sign bit flipped back per byte
+__device__ __forceinline__ uint32_t q8_pack4(float c0, float c1, float c2, float c3) {
+  uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(c0 + 128.f, 0, 0u);
+  w = __builtin_amdgcn_cvt_pk_u8_f32(c1 + 128.f, 1, w);
+  w = __builtin_amdgcn_cvt_pk_u8_f32(c2 + 128.f, 2, w);
+  w = __builtin_amdgcn_cvt_pk_u8_f32(c3 + 128.f, 3, w);
+  return w ^ 0x80808080u;
+}
+
 // max over the four 16-lane rows of a wave at the same column (lane ^ 16, ^ 32, ^ 48): two VALU
 // permlane swaps (v_permlane16_swap / v_permlane32_swap of a value with itself: results 0 / 1 hold
 // the row pair's two values) instead of three LDS bpermutes

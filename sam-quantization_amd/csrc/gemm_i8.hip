@@ -78,7 +78,8 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
 // through LDS in 32-row slices per wave (ep = this wave's 32 x WN f32 slice) so the global traffic
 // is row-contiguous 16-byte vectors.  Shared by the v3-style and the ping-pong int8 kernels.
 // ZPS: the sums exclude the zero point (acc = sum a * q) and the epilogue subtracts zp[n] * S[m]
-// (zpv = this lane's zp per column block, ssum = S of the wave's WM rows; int32-exact)
+// (zpv = MINUS this lane's zp per column block, ssum = S of the wave's WM rows; int32-exact, on
+// the full-rate 24-bit multiply: |zp| <= 16, |S| <= 128 K < 2^23)
 // Grouped W4 (float accumulators, the group scales already applied): wscale == nullptr, the
 // factor is a_scale alone.
 template <int TM, int TN, int WN, int EPI, bool ZPS = false, typename AccV = int16_t_v>
@@ -97,6 +98,7 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
   constexpr bool GELU = EPI == SAMQ_EPI_BIAS_GELU || EPI == SAMQ_EPI_Q8_GELU;
   const float inv_out = ep_args.out_scale > 0.f ? 1.0f / ep_args.out_scale : 0.f;   // q8_exact (common.h)
   const float inv_mid = ep_args.mid_scale > 0.f ? 1.0f / ep_args.mid_scale : 0.f;
+  const float lim_out = 130.0f * ep_args.out_scale, lim_mid = 130.0f * ep_args.mid_scale;   // q8_exact2 clamps
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -105,9 +107,9 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
         auto a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
-        if constexpr (ZPS) {
-          a0 -= zpv[t] * ssum[i * 32 + rl];
-          a1 -= zpv[t] * ssum[i * 32 + rl + 1];
+        if constexpr (ZPS) {   // v_mad_i32_i24 (zpv = -zp; |S| <= 128 K < 2^23: K < 65536 checked at launch)
+          a0 += __mul24(zpv[t], ssum[i * 32 + rl]);
+          a1 += __mul24(zpv[t], ssum[i * 32 + rl + 1]);
         }
         float2_t v = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]), (float2_t)(cb[t]));
         if (GELU) v = gelu_fast2(v);
@@ -168,19 +170,21 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
             u32x4 o;
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
-              uint32_t word = 0;
+              float cq[4];
 #pragma unroll
-              for (int b = 0; b < 4; ++b) {
-                float x = v[4 * w + b];
+              for (int b = 0; b < 4; b += 2) {
+                float2_t x = {v[4 * w + b], v[4 * w + b + 1]};
                 if (EPI == SAMQ_EPI_Q8_RES) {
-                  if (ep_args.mid_scale > 0.f) x = q8_exact(x, ep_args.mid_scale, inv_mid) * ep_args.mid_scale;
-                  const float rv = (float)(int8_t)((res[w] >> (8 * b)) & 0xFFu) * ep_args.res_scale;
+                  if (ep_args.mid_scale > 0.f) x = q8_exact2(x, ep_args.mid_scale, inv_mid, lim_mid) * ep_args.mid_scale;
+                  const float2_t rv = float2_t{(float)(int8_t)((res[w] >> (8 * b)) & 0xFFu),
+                                               (float)(int8_t)((res[w] >> (8 * b + 8)) & 0xFFu)} * ep_args.res_scale;
                   x = rv + x;
                 }
-                const int qv = (int)q8_exact(x, ep_args.out_scale, inv_out);
-                word |= ((uint32_t)qv & 0xFFu) << (8 * b);
+                const float2_t q = q8_exact2(x, ep_args.out_scale, inv_out, lim_out);
+                cq[b] = q.x;
+                cq[b + 1] = q.y;
               }
-              o[w] = word;
+              o[w] = q8_pack4(cq[0], cq[1], cq[2], cq[3]);
             }
             *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
           }
@@ -670,6 +674,15 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   }
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
 
+  if constexpr ((VAR & 32) != 0) {   // timing-only (tuning build): no epilogue, sums kept alive
+    int z = rsum;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int t = 0; t < TN; ++t) z += acc[i][t][0] + acc[i][t][15];
+    if (z == 123456789) ((int*)Cout)[tid] = z;
+    return;
+  }
   __syncthreads();
   if constexpr (ZPS) {
     int* s_lds = (int*)(smem + NW * EP_BYTES);
@@ -678,7 +691,7 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
     __syncthreads();
     int zpv[TN];
 #pragma unroll
-    for (int t = 0; t < TN; ++t) zpv[t] = (int)(zpx[t] & 0xFFu);
+    for (int t = 0; t < TN; ++t) zpv[t] = -(int)(zpx[t] & 0xFFu);
     i8_epilogue<TM, TN, WN, EPI, true>(acc, col, wscale, bias, ep_args, (float*)(smem + wave * EP_BYTES), Cout,
                                        ldc, M, m0 + wm * WM, n0 + wn * WN, lane, s_lds + wm * WM, zpv);
     return;
@@ -703,6 +716,8 @@ static int launch_i8(const I8Args& a, hipStream_t st) {
 
 template <int EPI, int STAGES, int LA, int VAR = 0>
 static int launch_i8_pp2(const I8Args& a, hipStream_t st) {
+  if constexpr ((VAR & 8) != 0)   // row sums on the 24-bit multiply (i8_epilogue ZPS)
+    SAMQ_REQUIRE(a.K < 65536, SAMQ_ERR_UNSUPPORTED, "w4a8_gemm: the row-sum zero-point path needs K < 65536");
   const int nwg = ((a.M + 255) / 256) * (a.N / 256);
   hipLaunchKernelGGL((i8_gemm_pp2<EPI, STAGES, LA, VAR>), dim3(nwg), dim3(512), 0, st, a.A, a.lda, a.Wp, a.wscale,
                      a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep);
@@ -726,6 +741,9 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 93 is the W4 ping-pong kernel");
 #ifdef SAMQ_TUNING
+    case 94:   // timing-only: cfg 86 without its epilogue
+      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 32>(a, st);
+      return fail(SAMQ_ERR_INVALID, "i8_gemm: W4 only");
     case 95: case 96: case 97:   // timing-only (wrong results): no zero point / no MFMA / no restaging
       if constexpr (BF == BF_W4) {
         if (cfg == 95) return launch_i8_pp2<EPI, 3, 2, 1>(a, st);
@@ -751,7 +769,7 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
+  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
     case 92: return 32; default: return 0; }
 }
 

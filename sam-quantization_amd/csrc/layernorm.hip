@@ -124,10 +124,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
           for (int e = 0; e < 4; ++e) o[e] = ln_q8(o[e], out_scale) * out_scale;
           ((float4_t*)y)[row * nvec + j] = o;
         } else if (OUT == LN_I8) {
-          uint32_t w = 0;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) w |= ((uint32_t)(int)ln_q8(o[e], out_scale) & 0xFFu) << (8 * e);
-          ((uint32_t*)y)[row * nvec + j] = w;
+          const float inv = 1.0f / out_scale, lim = 130.0f * out_scale;   // (loop-invariant: hoisted)
+          const float2_t c01 = q8_exact2(float2_t{o[0], o[1]}, out_scale, inv, lim);
+          const float2_t c23 = q8_exact2(float2_t{o[2], o[3]}, out_scale, inv, lim);
+          ((uint32_t*)y)[row * nvec + j] = q8_pack4(c01.x, c01.y, c23.x, c23.y);
         } else {
           ((half4_t*)y)[row * nvec + j] = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
         }

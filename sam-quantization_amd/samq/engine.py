@@ -214,7 +214,9 @@ class EncoderEngine:
         mark(0)
         p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
         mark(1)
-        ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8, out_scale=p.s_proj)
+        if ("win" if p.window else "glob") not in self.skip:
+            ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8,
+                              out_scale=p.s_proj)
         mark(2)
         if late:
             p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_F32, out=self._delta(bufs, torch.float32))

@@ -16,6 +16,12 @@ dev = torch.device("cuda:0")
 lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 VARIANTS = {"pick": {}, "res=ln32": {"res": "ln32"}}   # round 4: residual adds in the LayerNorm-q kernels
+if len(sys.argv) > 3:   # variants as "name:layer=cfg,res=ln32,skip_win=1;name:..." (pick always first)
+    VARIANTS = {"pick": {}}
+    for v in sys.argv[3].split(";"):
+        name, spec = v.split(":")
+        VARIANTS[name] = {kv.split("=")[0]: (kv.split("=")[1] if kv.split("=")[0] == "res" else int(kv.split("=")[1]))
+                          for kv in spec.split(",")}
 
 enc = random_quant_encoder("vit_h", -1, device=dev)
 enc.half()
@@ -28,6 +34,7 @@ img = torch.randn((8, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.res_mode = cfg.get("res", "epi")
+    eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).i8_cfg = cfg.get(lay, 0)

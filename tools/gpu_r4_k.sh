@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 4: packed exact int8 quantiser (q8_exact2 + q8_pack4) in the int8 GEMM / LN-q / attention
+# stores, offset-in-C-input global attention: exact-code tests, then bench A/B vs the previous build
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+o=gpurun_out/r4_k
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_w8a8.py tests/test_w4a8.py tests/test_gpu_kernels.py -m gpu -k "w8a8 or w4a8 or layernorm or rel_attention or quantize" > $o.tests.log 2>&1 || { tail -40 $o.tests.log; exit 1; }
+tail -2 $o.tests.log
+for r in 1 2; do
+  for lib in tools/ab/libsamq_prev.so new; do
+    if [ $lib = new ]; then unset SAMQ_LIB; else export SAMQ_LIB=$lib; fi
+    timeout -k 10 300 python -u bench.py --mode w4a8 --steps 10 --warmup 3 --no-cpu-baseline --no-isolated > $o.b48.$r.$(basename $lib).log 2>&1 || exit 1
+    echo "w4a8 $lib $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" $o.b48.$r.$(basename $lib).log)"
+    timeout -k 10 300 python -u bench.py --mode w8a8 --steps 20 --warmup 5 --no-cpu-baseline --no-isolated > $o.b88.$r.$(basename $lib).log 2>&1 || exit 1
+    echo "w8a8 $lib $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" $o.b88.$r.$(basename $lib).log)"
+    timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-isolated > $o.b16.$r.$(basename $lib).log 2>&1 || exit 1
+    echo "w4a16 $lib $(python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" $o.b16.$r.$(basename $lib).log)"
+  done
+done
