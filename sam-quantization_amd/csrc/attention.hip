@@ -893,10 +893,19 @@ template <int DBG>
 __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) {
   constexpr int D = 80, S = 64, KS = 5;
   constexpr int NSLOT = 5;                        // key-row ring slots
-  constexpr int ROWB = 20 * 1024;                 // one key row: K (10 KiB) | V (10 KiB)
-  constexpr int VB = 10 * 1024;
+  // ONESL (round 4; DBG & 512 = the round-3 layout): V of a key row as dims 0..63 (16 key quads x
+  // 512 B) | dims 64..79 (16 quads x 128 B) | 128 B pad | 2 KiB of fp16 ones written once per slot,
+  // so the lanes of d-block 2 that hold rows 80..95 (the softmax row sums) read 1.0 from LDS at
+  // their own base (+2176: the other 32 banks) instead of masking 4 dwords per P.V step.  Round 3:
+  // 16 key quads x (256 + 256 + 128 B) interleaved, rows 80..95 forced to 1.0 in registers.
+  constexpr bool ONESL = (DBG & 512) == 0;
+  constexpr int VB = 10 * 1024;                   // V dims 0..63 (ONESL) / all of V
+  constexpr int V2B = 18 * 1024;                  // ONESL: V dims 64..79
+  constexpr int ONESB = V2B + 2048 + 128;         // ONESL: the ones (+2176 from V2B)
+  constexpr int ROWB = ONESL ? ONESB + 2048 : 20 * 1024;   // one key row's ring slot
   constexpr int THB = 64 * 32 * 2;                // per wave: fp16 TH[kh][q]
   __shared__ __attribute__((aligned(16))) char smem[NSLOT * ROWB + 8 * THB];
+  static_assert(NSLOT * ROWB + 8 * THB <= 160 * 1024, "LDS");
   constexpr bool DBG_NOEXP = (DBG & 2) != 0, DBG_NOMFMA = (DBG & 4) != 0;
   // COFF (round 4): the next row's TH and softmax offset enter its Q.K^T as part of the C input
   // (C = TW + (TH[kh] - offset), a per-lane scalar added in the MFMA segment), so the softmax
@@ -907,6 +916,9 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   // the VALU segment; & 64 the first P.V step's V^T fragments read at the end of the VALU segment;
   // & 128 without PFENCE
   constexpr bool KEARLY = (DBG & 32) != 0, VPRE = (DBG & 64) != 0, PFENCE = (DBG & 128) == 0;
+  // & 256: CMFMA -- the per-row C offset (TH - offset) enters Q.K^T as one more MFMA k-step (ones x
+  // [hi; lo] of the offset, |c - hi - lo| <= 2^-22 |c|) instead of 32 adds to the C input
+  constexpr bool CMFMA = (DBG & 256) != 0 && COFF;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
   unsigned long long wgt[6] = {0, 0, 0, 0, 0, 0};
@@ -941,6 +953,18 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     if (v < 10) {                                  // K piece (kt, s): lane-linear A fragments
       key = 32 * (v / 5) + l32;
       dim = C + 16 * (v % 5) + 8 * h;
+    } else if (ONESL) {                            // V: dims 0..63 (pieces 10..17), 64..79 (18, 19)
+      const int gl = 64 * (v - 10) + lane;
+      if (v < 18) {                                // 16 key quads x (256 + 256 B)
+        const int kq = gl >> 5, w = gl & 31;
+        key = 4 * kq + ((w & 15) >> 2);
+        dim = 2 * C + 32 * (w >> 4) + 8 * (w & 3);
+      } else {                                     // 16 key quads x 128 B
+        const int g2 = gl - 512, kq = g2 >> 3, w = g2 & 7;
+        key = 4 * kq + (w >> 1);
+        dim = 2 * C + 64 + 8 * (w & 1);
+      }
+      key = key < S ? key : S - 1;
     } else {                                       // V: 16 key-quads x (256 + 256 + 128 bytes)
       const int gl = 64 * (v - 10) + lane;
       const int kq = gl / 40, w = gl % 40;
@@ -1008,9 +1032,16 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   // the g16 = 0 bytes and are forced to 1.0 below
   const int i16 = lane & 15, g16 = (lane >> 4) & 1;
   const int tq = i16 >> 2, tp = i16 & 3;
-  const uint32_t vb01 = lds_addr(smem + VB) + h * 640 + tq * 64 + g16 * 32 + tp * 8;
-  const uint32_t vb2 = lds_addr(smem + VB) + h * 640 + 512 + tq * 32 + tp * 8;
+  constexpr int QB = ONESL ? 512 : 640, QB2 = ONESL ? 128 : 640;   // bytes per key quad (dims 0..63 / 64..79)
+  const uint32_t vb01 = lds_addr(smem + VB) + h * QB + tq * 64 + g16 * 32 + tp * 8;
+  const uint32_t vb2 = ONESL ? lds_addr(smem + V2B) + h * QB2 + tq * 32 + tp * 8 + g16 * (ONESB - V2B)
+                             : lds_addr(smem + VB) + h * 640 + 512 + tq * 32 + tp * 8;
   const uint32_t ones_or = g16 ? 0x3C003C00u : 0u, ones_and = g16 ? 0u : 0xFFFFFFFFu;
+  if constexpr (ONESL) {   // the ones of every ring slot (read only after the barrier below)
+    const u32x4 one4 = {0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u};
+    for (int i = tid; i < NSLOT * 128; i += 512)
+      *(u32x4*)(smem + (i >> 7) * ROWB + ONESB + (i & 127) * 16) = one4;
+  }
 
   float16_t o[3];
 #pragma unroll
@@ -1027,11 +1058,20 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       for (int s = 0; s < KS; ++s) kf[kt][s] = *(const half8_t*)(kb + (kt * 5 + s) * 1024 + lane * 16);
   };
   float coff = 0.f;   // COFF: TH of the next row minus the offset baked into its scores
+  // CMFMA operands: A = ones in k-slots 0, 1 (lanes h = 0), B = [hi; lo] of coff in the same slots
+  const half8_t ones01 = h ? half8_t{} : half8_t{1, 1, 0, 0, 0, 0, 0, 0};
+  half8_t cq = {};
+  auto set_cq = [&] {
+    const _Float16 hi = (_Float16)coff;
+    const _Float16 lo = (_Float16)(coff - (float)hi);
+    cq = h ? half8_t{} : half8_t{hi, lo, 0, 0, 0, 0, 0, 0};
+  };
   auto qk = [&]() {   // S^T = K . Q^T + TW (COFF: + coff) for the two 32-key tiles of a key row
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       float16_t a = tw[kt];
-      if constexpr (COFF) a = a + coff;
+      if constexpr (CMFMA) a = mfma32(ones01, cq, a);
+      else if constexpr (COFF) a = a + coff;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         if (DBG_NOMFMA) a[s] += (float)kf[kt][s][0] * (float)qf[s][0];
@@ -1054,6 +1094,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   // row 0 whose m is -inf); the scores are then s + TH - moff and P = exp2(score)
   float moff = 0.f;
   if constexpr (COFF) coff = th_cur;
+  if constexpr (CMFMA) set_cq();
   auto softmax_coff = [&](int kh) {
     if (__any(pend)) {   // last row's deferred offset move (moff already includes it)
       const float alpha = pend ? __builtin_amdgcn_exp2f(m - m_pend) : 1.0f;
@@ -1106,6 +1147,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       th_cur = (float)thw[(kh + 1) * 32 + l32];
       moff = pend ? m_pend : m;
       coff = th_cur - moff;
+      if constexpr (CMFMA) set_cq();
     }
   };
   auto softmax = [&](int kh) {
@@ -1163,12 +1205,12 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   auto vread = [&](auto tc, uint32_t rb, half4_t (&lo)[3], half4_t (&hi)[3]) {
     constexpr int t = decltype(tc)::value;
     constexpr int KQ = 8 * (t >> 1) + 4 * (t & 1);   // key quad of slot j < 4 (+h); j >= 4: +2
-    lo[0] = ds_read_tr16_off<KQ * 640>(vb01 + rb);
-    hi[0] = ds_read_tr16_off<(KQ + 2) * 640>(vb01 + rb);
-    lo[1] = ds_read_tr16_off<KQ * 640 + 256>(vb01 + rb);
-    hi[1] = ds_read_tr16_off<(KQ + 2) * 640 + 256>(vb01 + rb);
-    lo[2] = ds_read_tr16_off<KQ * 640>(vb2 + rb);
-    hi[2] = ds_read_tr16_off<(KQ + 2) * 640>(vb2 + rb);
+    lo[0] = ds_read_tr16_off<KQ * QB>(vb01 + rb);
+    hi[0] = ds_read_tr16_off<(KQ + 2) * QB>(vb01 + rb);
+    lo[1] = ds_read_tr16_off<KQ * QB + 256>(vb01 + rb);
+    hi[1] = ds_read_tr16_off<(KQ + 2) * QB + 256>(vb01 + rb);
+    lo[2] = ds_read_tr16_off<KQ * QB2>(vb2 + rb);
+    hi[2] = ds_read_tr16_off<(KQ + 2) * QB2>(vb2 + rb);
   };
   half4_t vlo0[3], vhi0[3];   // VPRE: the t = 0 fragments, read in the VALU segment
   auto pv = [&](int slot) {   // O^T += V^T . P^T: 4 k16-steps x 3 d-blocks, next step's reads in flight
@@ -1194,7 +1236,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo[cb][0]), "+v"(hi[cb][0]), "+v"(lo[cb][1]), "+v"(hi[cb][1]),
                      "+v"(lo[cb][2]), "+v"(hi[cb][2]));
       }
-      {   // d-block 2, dims 80..95 -> 1.0 (row sums)
+      if constexpr (!ONESL) {   // d-block 2, dims 80..95 -> 1.0 (row sums)
         union { half4_t v; uint32_t w[2]; } a, c;
         a.v = lo[cb][2];
         c.v = hi[cb][2];
@@ -1255,6 +1297,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
                  "+v"(kf[0][1]), "+v"(kf[0][2]), "+v"(kf[0][3]), "+v"(kf[0][4]) :: "memory");
     asm volatile("" : "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[1][2]), "+v"(kf[1][3]), "+v"(kf[1][4]),
                  "+v"(o[0]), "+v"(o[1]), "+v"(o[2]) :: "memory");
+    if constexpr (CMFMA) asm volatile("" : "+v"(cq));
   };
   // ring slots as rotating wave-uniform counters (no per-row modulo); constant vmcnt counts per
   // group: group 0 (waves 0..3) issues 3 pieces per row, group 1 two
@@ -1353,6 +1396,10 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 8: hipLaunchKernelGGL(glob80_attention_kernel<8>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 512: hipLaunchKernelGGL(glob80_attention_kernel<512>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 256: hipLaunchKernelGGL(glob80_attention_kernel<256>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 288: hipLaunchKernelGGL(glob80_attention_kernel<288>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 320: hipLaunchKernelGGL(glob80_attention_kernel<320>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 32: hipLaunchKernelGGL(glob80_attention_kernel<32>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 64: hipLaunchKernelGGL(glob80_attention_kernel<64>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 96: hipLaunchKernelGGL(glob80_attention_kernel<96>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;

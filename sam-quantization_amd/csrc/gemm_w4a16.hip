@@ -1098,6 +1098,63 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
 }
 
 
+// f16-output epilogue staged TRANSPOSED (VAR & (1 << 22), round 4): per 32-row slice the wave
+// writes its 64 x 32 (column x row) f16 image -- lane (l32, hsel) packs the 4 consecutive rows of
+// one column that accumulator registers 4j .. 4j+3 hold into ONE ds_write_b64 (pitch 72 B: the 16
+// lanes of a write group on distinct banks) -- and reads it back row-contiguous with
+// ds_read_b64_tr_b16 (T10: lane 4q+p of a 16-lane group addresses image row q = output column, 4
+// output rows at 4p; lane i receives output row i, 4 columns), two reads per 16-byte store.  vs
+// pp_epilogue: 8 instead of 32 LDS writes per slice and half the staged bytes (f16, not f32).
+__device__ __forceinline__ half4_t ep_tr16(uint32_t addr) {
+  half4_t r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int TM, int TN, int EPI>
+__device__ __forceinline__ void pp_epilogue_f16t(const float16_t (&acc)[TM][TN], const float (&csc)[TN],
+                                                 const float (&cb)[TN], char* ep_bytes, void* Cout, int64_t ldc,
+                                                 int M, int row_base, int col_base, int lane) {
+  static_assert(TN == 2, "64-column wave tiles");
+  static_assert(EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU, "f16 outputs");
+  constexpr int PITCH = 72;                              // bytes per image row (32 f16 + 8 pad)
+  const int l32 = lane & 31, hsel = lane >> 5;
+  const uint32_t img = (uint32_t)(uintptr_t)((const SAMQ_LDS char*)ep_bytes);
+  // tr-read addresses: group g (lanes 16g..16g+15), iteration k: pair pi = 4k + g = (16-row half
+  // rb = pi & 1, 8-column chunk c8 = pi >> 1); lane 4q+p: image row 8 c8 + q (+4), rows 16 rb + 4p
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3, i16 = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float2_t v0 = __builtin_elementwise_fma((float2_t){acc[i][t][4 * j], acc[i][t][4 * j + 1]}, (float2_t)(csc[t]),
+                                                (float2_t)(cb[t]));
+        float2_t v1 = __builtin_elementwise_fma((float2_t){acc[i][t][4 * j + 2], acc[i][t][4 * j + 3]},
+                                                (float2_t)(csc[t]), (float2_t)(cb[t]));
+        if (EPI == SAMQ_EPI_BIAS_GELU) {
+          v0 = gelu_fast2(v0);
+          v1 = gelu_fast2(v1);
+        }
+        const half2_t h0 = __builtin_convertvector(v0, half2_t), h1 = __builtin_convertvector(v1, half2_t);
+        *(half4_t*)(ep_bytes + (32 * t + l32) * PITCH + (8 * j + 4 * hsel) * 2) = half4_t{h0.x, h0.y, h1.x, h1.y};
+      }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice image is in LDS
+    const int srow0 = row_base + i * 32;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pi = 4 * k + g, rb = pi & 1, c8 = pi >> 1;
+      const uint32_t a = img + (8 * c8 + q) * PITCH + (16 * rb + 4 * pp) * 2;
+      half4_t lo = ep_tr16(a), hi = ep_tr16(a + 4 * PITCH);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
+      const int row = srow0 + 16 * rb + i16;
+      if (row < M)
+        *(half8_t*)((_Float16*)Cout + (int64_t)row * ldc + col_base + 8 * c8) =
+            half8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  }
+}
+
 // Direct epilogue of a TRANSPOSED accumulator (VAR & 128: the MFMA is issued as W^T . A^T, so a
 // lane's accumulator registers run along N): every lane holds G consecutive output columns of ONE
 // row per register group and stores them straight from registers (G = 4: 8 bytes of fp16 or 16
@@ -1740,6 +1797,12 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   if constexpr (lnf_consumer(EPI))
     lnf_rowinfo_wg<BM, NW>(lnf, (float2_t*)(smem + NW * EP_BYTES), smem + NW * EP_BYTES + RI_BYTES, M, m0, n0 == 0,
                            wave, lane);
+  if constexpr ((VAR & (1 << 22)) != 0) {
+    static_assert(EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU, "transposed f16 staging: f16 outputs");
+    static_assert(EP_BYTES >= 64 * 72, "transposed f16 staging image");
+    pp_epilogue_f16t<TM, TN, EPI>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM, n0 + wn * WN, lane);
+    return;
+  }
   pp_epilogue<TM, TN, EP_ROWS, EPI, (VAR >> 17) & 3>(acc, csc, cb, smem + wave * EP_BYTES, Cout, ldc, M, m0 + wm * WM,
                                                      n0 + wn * WN, lane, lnf, N, rowinfo);
 }
@@ -1878,6 +1941,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 107: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 20)>(a, st);
       // cfg 57 / 64 with the epilogue's scale / bias loaded before the prologue (VAR & (1 << 21))
       case 109: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 21)>(a, st);
+      // cfg 57 with the transposed f16 staging epilogue (f16 outputs; f32 outputs take cfg 57's)
+      case 111:
+        if constexpr (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 22)>(a, st);
+        else return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
       case 110: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | (1 << 21)>(a, st);
       case 108: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | (1 << 20)>(a, st);
       // cfg 57 with transposed accumulators and the f16-staged epilogue (f16 outputs only)
@@ -2029,7 +2096,7 @@ static int cfg_bn(int cfg) {
                  case 74: case 75: case 76: case 77: case 78: case 79: return 256;
                  case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
                  case 97: case 98: return 512;
-                 case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109: case 110: return 256;
+                 case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109: case 110: case 111: return 256;
                  default: return 0; }
 }
 

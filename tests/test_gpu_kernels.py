@@ -98,7 +98,7 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
         _close(ops.w4a16_gemm(*args, ops.EPI_F32, cfg=cfg), y, 2e-5 if groupsize == -1 else 4e-3)
 
 
-@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101, 104, 107, 108, 109, 110])
+@pytest.mark.parametrize("cfg", [55, 56, 57, 58, 62, 64, 65, 100, 101, 104, 107, 108, 109, 110, 111])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
@@ -115,11 +115,12 @@ def test_w4a16_gemm_pingpong(cuda, cfg, epi):
         _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, -1, epi, cfg, rng)
 
 
-@pytest.mark.parametrize("cfg,base", [(107, 57), (108, 64)])
+@pytest.mark.parametrize("cfg,base", [(107, 57), (108, 64), (111, 57)])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_persistent_matches(cuda, cfg, base, epi):
     """The persistent ping-pong form (one workgroup per CU looping over the tiles) computes every
-    tile exactly like its one-tile-per-workgroup twin: bit-identical at M = 16384, N = 1280
+    tile exactly like its one-tile-per-workgroup twin, and cfg 111 (cfg 57 with the transposed
+    f16-staged epilogue) like cfg 57: bit-identical at M = 16384, N = 1280
     (320 tiles on <= 256 workgroups, so workgroups run two tiles) and at a ragged M."""
     from samq import ops
     for m, k, n in ((16384, 1280, 1280), (9000, 640, 768)):
