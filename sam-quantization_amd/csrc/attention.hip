@@ -531,7 +531,10 @@ __global__ __launch_bounds__(64 * NW, 1) void rel_attention_kernel(AttnParams p)
 // softmax's exp2 argument (one fma per score, as the subtraction it replaces): no fp16 rounding of
 // q * scale * log2e (a 2^-12 relative error on every score), and TH rounded to fp16 where the
 // reference rounds rel_h (q . Rh, unscaled)
-template <int D, bool UNSC = false>
+// PHL (round 4, the W4A8 int8-code store): P enters P.V as fp16 hi + lo (P - hi, |P - hi - lo| ~
+// 2^-22 |P|, attention_q8.hip's split) -- two MFMAs per P.V step and for the row sums -- so the
+// output carries fp32-level error instead of fp16 P's 2^-12, before the proj QAct's quantiser
+template <int D, bool UNSC = false, bool PHL = false>
 struct Win {
   static constexpr int S = 14, QT = 2;
   static constexpr int KS = D == 80 ? 3 : 2;            // k32 steps of Q.K^T
@@ -711,6 +714,7 @@ struct Win {
 
     // ---- exact softmax over the window (exp2 domain)
     half8_t pb[QT][S / 2];
+    half8_t pl[PHL ? QT : 1][PHL ? S / 2 : 1];   // PHL: the lo parts
 #pragma unroll
     for (int t = 0; t < QT; ++t) {
       // two independent max3 chains (no canonicalising v_max of a lone fmaxf)
@@ -726,7 +730,18 @@ struct Win {
       }
       mx = fmaxf(mx, my);
       mx = max_rows4(mx);
-      if constexpr (UNSC) {   // P = exp2((S_u - max) * scale * log2e) as one fma per score
+      if constexpr (UNSC && PHL) {
+        const float nmx = -mx * qscale;
+#pragma unroll
+        for (int pr = 0; pr < S / 2; ++pr)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(sc[t][2 * pr + (r >> 2)][r & 3], qscale, nmx));
+            const _Float16 hi = (_Float16)e;
+            pb[t][pr][r] = hi;
+            pl[PHL ? t : 0][PHL ? pr : 0][r] = (_Float16)(e - (float)hi);
+          }
+      } else if constexpr (UNSC) {   // P = exp2((S_u - max) * scale * log2e) as one fma per score
         const float nmx = -mx * qscale;
 #pragma unroll
         for (int pr = 0; pr < S / 2; ++pr)
@@ -794,12 +809,16 @@ struct Win {
         const half8_t va = {vlo[cb][d][0], vlo[cb][d][1], vlo[cb][d][2], vlo[cb][d][3],
                             vhi[cb][d][0], vhi[cb][d][1], vhi[cb][d][2], vhi[cb][d][3]};
 #pragma unroll
-        for (int t = 0; t < QT; ++t)
+        for (int t = 0; t < QT; ++t) {
           o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[t][pr], pr ? o[t][d] : zero4, 0, 0, 0);
+          if constexpr (PHL) o[t][d] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pl[t][pr], o[t][d], 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int t = 0; t < QT; ++t)
+      for (int t = 0; t < QT; ++t) {
         lsum[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pb[t][pr], pr ? lsum[t] : zero4, 0, 0, 0);
+        if constexpr (PHL) lsum[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, pl[t][pr], lsum[t], 0, 0, 0);
+      }
     });
 
     // ---- normalise + store (token-major [B, H, W, C])
@@ -818,9 +837,9 @@ struct Win {
 // One item per 4-wave workgroup, two workgroups per CU (rows 2w, 2w+1 then 8+2w, 9+2w).  (A
 // persistent form -- one 8-wave workgroup per CU, wave 7 streaming the next item's K/V into a second
 // buffer while waves 0..6 compute -- measured 37.9 vs 37.0 us per 2-image ViT-H launch.)
-template <int D, bool UNSC = false>
+template <int D, bool UNSC = false, bool PHL = false>
 __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int items) {
-  using W = Win<D, UNSC>;
+  using W = Win<D, UNSC, PHL>;
   static_assert(W::KVB + W::TABB <= 80 * 1024, "two workgroups per CU");
   __shared__ __attribute__((aligned(16))) char smem[W::KVB + W::TABB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -919,6 +938,13 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   // & 256: CMFMA -- the per-row C offset (TH - offset) enters Q.K^T as one more MFMA k-step (ones x
   // [hi; lo] of the offset, |c - hi - lo| <= 2^-22 |c|) instead of 32 adds to the C input
   constexpr bool CMFMA = (DBG & 256) != 0 && COFF;
+  // & 1024: G1DMA -- group 1 alone issues all 20 pieces of row kh+4, 5 per wave, in its VALU
+  // segment of row kh (after its exp2s; the LDS-DMA issue is cheap among VALU, dear inside an MFMA
+  // burst, MI355X_MICROARCH.md constants); group 0's MFMA segments carry no DMA
+  constexpr bool G1DMA = (DBG & 1024) != 0;
+  // & 2048: STATPRIO -- group 1 (the younger half) at s_setprio 1 for the whole loop, no
+  // per-segment priority flips (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
+  constexpr bool STATPRIO = (DBG & 2048) != 0;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
   unsigned long long wgt[6] = {0, 0, 0, 0, 0, 0};
@@ -942,13 +968,14 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   const _Float16* img = p.qkv + (int64_t)b * S * S * p.tok_stride;
 
   // ---- K / V staging: 20 pieces per key row; wave w issues pieces w, w + 8 (, w + 16 for w < 4)
-  constexpr int NI = 3;
-  const int npc = wave < 4 ? 3 : 2;
+  // (G1DMA: group 1's wave 4 + u issues pieces u, u + 4, .., u + 16)
+  constexpr int NI = G1DMA ? 5 : 3;
+  const int npc = G1DMA ? (grp ? 5 : 0) : (wave < 4 ? 3 : 2);
   const _Float16* src0[NI];
   int dst[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int v = wave + 8 * i;
+    const int v = G1DMA ? (wave & 3) + 4 * i : wave + 8 * i;
     int key, dim;
     if (v < 10) {                                  // K piece (kt, s): lane-linear A fragments
       key = 32 * (v / 5) + l32;
@@ -1301,8 +1328,11 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   };
   // ring slots as rotating wave-uniform counters (no per-row modulo); constant vmcnt counts per
   // group: group 0 (waves 0..3) issues 3 pieces per row, group 1 two
-  static_assert(NI == 3, "vmcnt counts below: 3 / 2 pieces per row for group 0 / 1");
+  static_assert(NI == (G1DMA ? 5 : 3), "vmcnt counts below: 3 / 2 pieces per row for group 0 / 1 (G1DMA: 0 / 5)");
   int j = 0;   // kh % NSLOT
+  if constexpr (STATPRIO) {
+    if (grp) __builtin_amdgcn_s_setprio(1);
+  }
   for (int kh = 0; kh < S; ++kh) {
     const int j1 = j == NSLOT - 1 ? 0 : j + 1, j4 = j == 0 ? NSLOT - 1 : j - 1;
     stamp(3);
@@ -1311,6 +1341,9 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       if (kh + 1 < S) kread(smem + j1 * ROWB);
     }
     softmax(kh);
+    if constexpr (G1DMA) {   // row kh+4 into row kh-1's slot: every P.V of row kh-1 ended at barrier 2kh
+      if (grp && kh + 4 < S) issue(kh + 4, j4);
+    }
     if constexpr (!KEARLY) {
       if (kh + 1 < S) kread(smem + j1 * ROWB);
     }
@@ -1319,7 +1352,13 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     fence_pk();
     if constexpr (VPRE)
       asm volatile("" : "+v"(vlo0[0]), "+v"(vlo0[1]), "+v"(vlo0[2]), "+v"(vhi0[0]), "+v"(vhi0[1]), "+v"(vhi0[2]));
-    if (grp && kh + 2 < S) {   // row kh+2 (row kh+3 newer)
+    if constexpr (G1DMA) {
+      if (grp && kh + 2 < S) {   // row kh+2 (rows kh+3, kh+4 newer), read by group 0 after barrier 2kh+1
+        if (kh + 4 < S) wait_vmcnt<10>();
+        else if (kh + 3 < S) wait_vmcnt<5>();
+        else wait_vmcnt<0>();
+      }
+    } else if (grp && kh + 2 < S) {   // row kh+2 (row kh+3 newer)
       if (kh + 3 < S) wait_vmcnt<2>();
       else wait_vmcnt<0>();
     }
@@ -1329,13 +1368,13 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     __builtin_amdgcn_sched_barrier(0);
     stamp(1);
     fence_pk();
-    __builtin_amdgcn_s_setprio(1);
-    if (kh + 4 < S) issue(kh + 4, j4);
+    if constexpr (!STATPRIO) __builtin_amdgcn_s_setprio(1);
+    if (!G1DMA && kh + 4 < S) issue(kh + 4, j4);
     pv(j);
     if (kh + 1 < S) qk();
     fence_sc();
-    __builtin_amdgcn_s_setprio(0);
-    if (!grp && kh + 2 < S) {   // row kh+2 (rows kh+3, kh+4 newer)
+    if constexpr (!STATPRIO) __builtin_amdgcn_s_setprio(0);
+    if (!G1DMA && !grp && kh + 2 < S) {   // row kh+2 (rows kh+3, kh+4 newer)
       if (kh + 4 < S) wait_vmcnt<6>();
       else if (kh + 3 < S) wait_vmcnt<3>();
       else wait_vmcnt<0>();
@@ -1352,6 +1391,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     for (int k = 0; k < 4; ++k) atomicAdd(&g_attn_stamps[k + (grp ? 4 : 0)], ph[k]);
   }
 #endif
+  if constexpr (STATPRIO) __builtin_amdgcn_s_setprio(0);
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
   wg_mark<DBG>(wgt, 2);
 
@@ -1396,6 +1436,13 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 8: hipLaunchKernelGGL(glob80_attention_kernel<8>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 2048: hipLaunchKernelGGL(glob80_attention_kernel<2048>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 2304: hipLaunchKernelGGL(glob80_attention_kernel<2304>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 257: hipLaunchKernelGGL(glob80_attention_kernel<257>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 1024: hipLaunchKernelGGL(glob80_attention_kernel<1024>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 1280: hipLaunchKernelGGL(glob80_attention_kernel<1280>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 1025: hipLaunchKernelGGL(glob80_attention_kernel<1025>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 1032: hipLaunchKernelGGL(glob80_attention_kernel<1032>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 512: hipLaunchKernelGGL(glob80_attention_kernel<512>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 256: hipLaunchKernelGGL(glob80_attention_kernel<256>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 288: hipLaunchKernelGGL(glob80_attention_kernel<288>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
@@ -1457,14 +1504,23 @@ template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
 #ifdef SAMQ_TUNING
-  const char* e = getenv("SAMQ_ATTN_WIN");   // tuning A/B: 1 = the unscaled-Q variant (Win UNSC)
-  if (e && atoi(e) == 1) {
-    hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
+  // tuning A/B: 2 = the round-3 scaled-Q form (Win !UNSC); 3 = the int8 store without PHL
+  const char* e = getenv("SAMQ_ATTN_WIN");
+  if (e && (atoi(e) == 2 || atoi(e) == 3)) {
+    if (atoi(e) == 2) hipLaunchKernelGGL((win_attention_kernel<D, false>), dim3(items), dim3(256), 0, stream, p, items);
+    else hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
     SAMQ_LAUNCH_CHECK("win_attention launch");
     return SAMQ_OK;
   }
 #endif
-  hipLaunchKernelGGL((win_attention_kernel<D>), dim3(items), dim3(256), 0, stream, p, items);
+  if (p.out_scale > 0.f) {   // W4A8: int8 codes of the f32 output, P as hi + lo
+    hipLaunchKernelGGL((win_attention_kernel<D, true, true>), dim3(items), dim3(256), 0, stream, p, items);
+    SAMQ_LAUNCH_CHECK("win_attention launch");
+    return SAMQ_OK;
+  }
+  // unscaled Q (UNSC): 35.6 vs 36.2 us per ViT-H 2-image launch, fp16 output 1.59e-3 vs 1.95e-3
+  // max-abs from the fp32 oracle, W4A8 store codes off by one 1.7e-3 vs 2.5e-3 (profiles/r4_m.win.log)
+  hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
   SAMQ_LAUNCH_CHECK("win_attention launch");
   return SAMQ_OK;
 }

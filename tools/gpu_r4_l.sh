@@ -14,7 +14,7 @@ SAMQ_LIB=tuning timeout -k 10 120 python -u tools/attn_variant_ab.py 0,8 2 1 > $
 tail -9 $o.tl.log
 SAMQ_LIB=tools/ab/libsamq_prev.so timeout -k 10 120 python -u tools/attn_variant_ab.py 0 2 6 > $o.gprev.log 2>&1 || { tail -20 $o.gprev.log; exit 1; }
 cat $o.gprev.log
-SAMQ_LIB=tuning timeout -k 10 200 python -u tools/attn_variant_ab.py 0,128,32,64,96,16 2 8 > $o.gvar.log 2>&1 || { tail -20 $o.gvar.log; exit 1; }
+SAMQ_LIB=tuning timeout -k 10 200 python -u tools/attn_variant_ab.py 0,512,128,32,64,256,288,16 2 8 > $o.gvar.log 2>&1 || { tail -20 $o.gvar.log; exit 1; }
 cat $o.gvar.log
 for r in 1; do
   for lib in tools/ab/libsamq_prev.so new; do

@@ -48,3 +48,21 @@ for _ in range(rounds):
 for v in variants:
     ts = sorted(times[v])
     print(f"window variant {v}: median {ts[len(ts) // 2]:.2f} us  min {ts[0]:.2f} us", flush=True)
+# the int8-code store (W4A8 proj input): timing per variant
+out8 = torch.empty(qkv16.shape[:3] + (1280,), dtype=torch.int8, device=dev)
+t8 = {v: [] for v in variants}
+for _ in range(rounds):
+    for v in variants:
+        os.environ["SAMQ_ATTN_WIN"] = str(v)
+        for _ in range(2):
+            ops.rel_attention(*args, out_scale=s, out=out8)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            ops.rel_attention(*args, out_scale=s, out=out8)
+        e1.record()
+        torch.cuda.synchronize()
+        t8[v].append(e0.elapsed_time(e1) / 20 * 1e3)
+for v in variants:
+    ts = sorted(t8[v])
+    print(f"window variant {v} int8 store: median {ts[len(ts) // 2]:.2f} us  min {ts[0]:.2f} us", flush=True)
