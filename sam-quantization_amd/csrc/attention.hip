@@ -945,6 +945,9 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
   // & 2048: STATPRIO -- group 1 (the younger half) at s_setprio 1 for the whole loop, no
   // per-segment priority flips (MI355X_MICROARCH.md "Two waves per SIMD" item 4)
   constexpr bool STATPRIO = (DBG & 2048) != 0;
+  // & 4096: QKDMA -- the row's LDS-DMA pieces issued between the Q.K^T MFMAs (no LDS reads in
+  // flight there) instead of ahead of the P.V step's V^T reads
+  constexpr bool QKDMA = (DBG & 4096) != 0;
 
   _Float16* th_lds = (_Float16*)(smem + NSLOT * ROWB);
   unsigned long long wgt[6] = {0, 0, 0, 0, 0, 0};
@@ -1004,12 +1007,14 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     dst[i] = v * 1024;
   }
   const int64_t rowstride = (int64_t)S * p.tok_stride;
+  auto issue_one = [&](int kh, int slot, int i) {
+    if (i < npc)
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src0[i] + kh * rowstride),
+                                       (SAMQ_LDS void*)(smem + slot * ROWB + dst[i]), 16, 0, 0);
+  };
   auto issue = [&](int kh, int slot) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
-      if (i < npc)
-        __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)(src0[i] + kh * rowstride),
-                                         (SAMQ_LDS void*)(smem + slot * ROWB + dst[i]), 16, 0, 0);
+    for (int i = 0; i < NI; ++i) issue_one(kh, slot, i);
   };
 #pragma unroll
   for (int r = 0; r < NSLOT - 1; ++r) issue(r, r);
@@ -1093,7 +1098,8 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     const _Float16 lo = (_Float16)(coff - (float)hi);
     cq = h ? half8_t{} : half8_t{hi, lo, 0, 0, 0, 0, 0, 0};
   };
-  auto qk = [&]() {   // S^T = K . Q^T + TW (COFF: + coff) for the two 32-key tiles of a key row
+  // dma(i): QKDMA's piece issue after the i-th Q.K^T MFMA (i = 0..9; pieces at i = 1, 4, 7)
+  auto qk_d = [&](auto&& dma) {   // S^T = K . Q^T + TW (COFF: + coff) for the two 32-key tiles of a key row
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       float16_t a = tw[kt];
@@ -1103,10 +1109,12 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
       for (int s = 0; s < KS; ++s) {
         if (DBG_NOMFMA) a[s] += (float)kf[kt][s][0] * (float)qf[s][0];
         else a = mfma32(kf[kt][s], qf[s], a);
+        dma(KS * kt + s);
       }
       sc[kt] = a;
     }
   };
+  auto qk = [&]() { qk_d([](int) {}); };
   // Online softmax (exp2 domain), lane = one query, 32 of its 64 keys.  P is computed with the
   // offset m of the PREVIOUS rows, so the exp2s do not wait for this row's max (whose reduction +
   // cross-lane step + compare is a serial chain): the max runs beside them and only decides
@@ -1369,9 +1377,24 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
     stamp(1);
     fence_pk();
     if constexpr (!STATPRIO) __builtin_amdgcn_s_setprio(1);
-    if (!G1DMA && kh + 4 < S) issue(kh + 4, j4);
+    if (!G1DMA && !QKDMA && kh + 4 < S) issue(kh + 4, j4);
     pv(j);
-    if (kh + 1 < S) qk();
+    if constexpr (QKDMA) {
+      const bool pf = kh + 4 < S;
+      if (kh + 1 < S) {
+        qk_d([&](int q) {
+          if (pf && (q == 1 || q == 4 || q == 7)) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue_one(kh + 4, j4, q / 3);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        });
+      } else if (pf) {
+        issue(kh + 4, j4);
+      }
+    } else if (kh + 1 < S) {
+      qk();
+    }
     fence_sc();
     if constexpr (!STATPRIO) __builtin_amdgcn_s_setprio(0);
     if (!G1DMA && !grp && kh + 2 < S) {   // row kh+2 (rows kh+3, kh+4 newer)
@@ -1436,6 +1459,8 @@ static int launch_glob80(const AttnParams& p, int units, hipStream_t stream) {
     case 4: hipLaunchKernelGGL(glob80_attention_kernel<4>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 6: hipLaunchKernelGGL(glob80_attention_kernel<6>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 8: hipLaunchKernelGGL(glob80_attention_kernel<8>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 4096: hipLaunchKernelGGL(glob80_attention_kernel<4096>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
+    case 4097: hipLaunchKernelGGL(glob80_attention_kernel<4097>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 2048: hipLaunchKernelGGL(glob80_attention_kernel<2048>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 2304: hipLaunchKernelGGL(glob80_attention_kernel<2304>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
     case 257: hipLaunchKernelGGL(glob80_attention_kernel<257>, dim3(16 * p.heads * units), dim3(512), 0, stream, q); break;
@@ -1504,20 +1529,17 @@ template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
 #ifdef SAMQ_TUNING
-  // tuning A/B: 2 = the round-3 scaled-Q form (Win !UNSC); 3 = the int8 store without PHL
+  // tuning A/B: 2 = the round-3 scaled-Q form (Win !UNSC); 4 = the int8 store with P as hi + lo
+  // (PHL: W4A8 window-stage codes off by one 1.2-1.3e-3 vs 2.1-2.2e-3, but the int8-store launch
+  // 45.4 vs 35.5 us and the W4A8 step 35.7 vs 35.1 ms, profiles/r4_o.*: not the product path)
   const char* e = getenv("SAMQ_ATTN_WIN");
-  if (e && (atoi(e) == 2 || atoi(e) == 3)) {
+  if (e && (atoi(e) == 2 || atoi(e) == 4)) {
     if (atoi(e) == 2) hipLaunchKernelGGL((win_attention_kernel<D, false>), dim3(items), dim3(256), 0, stream, p, items);
-    else hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
+    else hipLaunchKernelGGL((win_attention_kernel<D, true, true>), dim3(items), dim3(256), 0, stream, p, items);
     SAMQ_LAUNCH_CHECK("win_attention launch");
     return SAMQ_OK;
   }
 #endif
-  if (p.out_scale > 0.f) {   // W4A8: int8 codes of the f32 output, P as hi + lo
-    hipLaunchKernelGGL((win_attention_kernel<D, true, true>), dim3(items), dim3(256), 0, stream, p, items);
-    SAMQ_LAUNCH_CHECK("win_attention launch");
-    return SAMQ_OK;
-  }
   // unscaled Q (UNSC): 35.6 vs 36.2 us per ViT-H 2-image launch, fp16 output 1.59e-3 vs 1.95e-3
   // max-abs from the fp32 oracle, W4A8 store codes off by one 1.7e-3 vs 2.5e-3 (profiles/r4_m.win.log)
   hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);

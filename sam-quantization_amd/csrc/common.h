@@ -84,6 +84,30 @@ __device__ __forceinline__ float2_t gelu_fast2(float2_t x) {
   return __builtin_elementwise_fma(-ax, poly * e, m);
 }
 
+// GELU on two values with erf from Abramowitz & Stegun 7.1.28, erf(z) = 1 - (1 + a1 z + .. + a6 z^6)^-16
+// (|error of erf| <= 3e-7): no exp2, one v_rcp, the 16th power as four packed squarings; 1/sqrt2
+// and 2^(1/16) folded into the coefficients so r = 0.5 / p^16 directly and
+//   GELU(x) = relu(x) - |x| r.
+// 11 packed + 4 plain VALU + 2 v_rcp per pair (gelu_fast2: 10 + 4 + 2 v_rcp + 2 v_exp; the
+// transcendentals issue at 8 cycles).  Max |error| against the exact erf form 7.1e-7 over
+// [-15, 15] (fp32 emulation) -- twice gelu_fast's, far below an int8 code step or an fp16 ulp.
+__device__ __forceinline__ float2_t gelu_r16_2(float2_t x) {
+  const float2_t ax = __builtin_elementwise_abs(x);
+  float2_t p = __builtin_elementwise_fma((float2_t)(5.6212996640e-06f), ax, (float2_t)(5.1055209009e-05f));
+  p = __builtin_elementwise_fma(p, ax, (float2_t)(3.9686137011e-05f));
+  p = __builtin_elementwise_fma(p, ax, (float2_t)(3.4227392389e-03f));
+  p = __builtin_elementwise_fma(p, ax, (float2_t)(2.2076998457e-02f));
+  p = __builtin_elementwise_fma(p, ax, (float2_t)(5.2075163037e-02f));
+  p = __builtin_elementwise_fma(p, ax, (float2_t)(1.0442737824e+00f));
+  p = p * p;
+  p = p * p;
+  p = p * p;
+  p = p * p;
+  const float2_t r = {__builtin_amdgcn_rcpf(p.x), __builtin_amdgcn_rcpf(p.y)};
+  const float2_t m = {fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)};
+  return __builtin_elementwise_fma(-ax, r, m);
+}
+
 // clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
 // quantizer/uniform.py:31-36), branch-free.  q0 = fl(v * inv) with inv = fl(1/s) can be ~1.5 ulp
 // off v/s -- outside Markstein's precondition (a faithful q) -- so one correction is not provably

@@ -99,6 +99,18 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
   const float inv_out = ep_args.out_scale > 0.f ? 1.0f / ep_args.out_scale : 0.f;   // q8_exact (common.h)
   const float inv_mid = ep_args.mid_scale > 0.f ? 1.0f / ep_args.mid_scale : 0.f;
   const float lim_out = 130.0f * ep_args.out_scale, lim_mid = 130.0f * ep_args.mid_scale;   // q8_exact2 clamps
+  // staging swizzle (round 4): the readers below take 64 B (int8 path: 16 columns, 4 ds_read_b128)
+  // or 32 B (f16 path: 8 columns, 2 reads) of one row per lane, and a ds_read_b128 lane group
+  // spans 4 rows whose k-th 16-byte chunks sat on the same banks (PMC: 3.9 M conflict cycles per
+  // W4A8 lin1 launch at M = 16384, profiles/r4_pmc_i8_pp2_m16384.txt).  Column c of slice row r is
+  // stored at c ^ swz(r), swz = 4 * key: the 4-column chunk within each 16 (int8) / 8 (f16)
+  // columns XOR key = (r >> 1) & 3 / & 1, so read k of the group's rows lands on distinct banks;
+  // rows r, r + 1 (r even) share the key, so a lane's accumulator pair still stores with one
+  // ds_write2
+  constexpr bool Q8OUT = EPI == SAMQ_EPI_Q8 || EPI == SAMQ_EPI_Q8_GELU || EPI == SAMQ_EPI_Q8_RES;
+  constexpr bool F16OUT = EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU;
+  constexpr int SWZ = (Q8OUT && WN % 16 == 0) ? 1 : (F16OUT && WN % 8 == 0) ? 2 : 0;
+  auto swz = [](int row) { return SWZ == 1 ? 4 * ((row >> 1) & 3) : SWZ == 2 ? 4 * ((row >> 1) & 1) : 0; };
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -112,9 +124,10 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
           a1 += __mul24(zpv[t], ssum[i * 32 + rl + 1]);
         }
         float2_t v = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]), (float2_t)(cb[t]));
-        if (GELU) v = gelu_fast2(v);
-        ep[rl * WN + t * 32 + (lane & 31)] = v.x;
-        ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
+        if (GELU) v = gelu_r16_2(v);
+        const int cs = (t * 32 + (lane & 31)) ^ swz(rl);   // rl even: swz(rl + 1) == swz(rl)
+        ep[rl * WN + cs] = v.x;
+        ep[(rl + 1) * WN + cs] = v.y;
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -139,8 +152,9 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
         if (idx < 32 * C8) {
           const int rl = idx / C8, c8 = idx % C8;
           const int row = row_base + i * 32 + rl;
-          const float4_t v0 = ((const float4_t*)ep)[2 * idx];
-          const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+          const int f4 = rl * (WN / 4) + 2 * c8, sk = swz(rl) / 4;   // float4s of the 8 columns
+          const float4_t v0 = ((const float4_t*)ep)[f4 + sk];
+          const float4_t v1 = ((const float4_t*)ep)[f4 + (1 ^ sk)];
           if (row < M) {
             const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
                                (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};
@@ -158,9 +172,10 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
           const int row = row_base + i * 32 + rl;
           if (row < M) {
             float v[16];
+            const int f4 = rl * (WN / 4) + 4 * c16, sk = swz(rl) / 4;   // float4s of the 16 columns
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float4_t f = ((const float4_t*)ep)[4 * idx + e];
+              const float4_t f = ((const float4_t*)ep)[f4 + (e ^ sk)];
               v[4 * e] = f[0]; v[4 * e + 1] = f[1]; v[4 * e + 2] = f[2]; v[4 * e + 3] = f[3];
             }
             u32x4 res;

@@ -980,6 +980,7 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
   static_assert(!(lnf_producer(EPI) || lnf_consumer(EPI)) || WN == 64, "LN fold: 64-column wave tiles");
   float* ep = (float*)ep_bytes;
   const int hsel = lane >> 5;
+  constexpr bool F16SWZ = EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU;   // staging swizzle (below)
   if constexpr (EPI == SAMQ_EPI_SILU_MUL) {
     // gated MLP: the wave's 64 columns are one 32-column block of the gate (t = 0) and the same
     // block of the up projection (t = 1) -- samq_w4_interleave32 layout; out f16 [M, N / 2] =
@@ -1035,8 +1036,11 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
                                   : __builtin_elementwise_fma((float2_t){acc[i][t][r], acc[i][t][r + 1]}, (float2_t)(csc[t]),
                                                               (float2_t)(lnf_consumer(EPI) ? 0.0f : cb[t]));
           if (EPI == SAMQ_EPI_BIAS_GELU && !(EVAR & 2)) v = gelu_fast2(v);
-          ep[rl * WN + t * 32 + (lane & 31)] = v.x;
-          ep[(rl + 1) * WN + t * 32 + (lane & 31)] = v.y;
+          // f16 outputs: the 4-column chunk XOR ((rl >> 1) & 1) within each 8 columns, so the two
+          // 16-byte reads of a lane group's 4 rows land on distinct banks (gemm_i8.hip i8_epilogue)
+          const int cs = (t * 32 + (lane & 31)) ^ (F16SWZ ? 4 * ((rl >> 1) & 1) : 0);
+          ep[rl * WN + cs] = v.x;
+          ep[(rl + 1) * WN + cs] = v.y;
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slice is in LDS (same wave reads it)
@@ -1082,8 +1086,9 @@ __device__ __forceinline__ void pp_epilogue(const float16_t (&acc)[TM][TN], cons
           if (idx < EP_ROWS * C8) {
             const int rl = idx / C8, c8 = idx % C8;
             const int row = srow0 + rl;
-            const float4_t v0 = ((const float4_t*)ep)[2 * idx];
-            const float4_t v1 = ((const float4_t*)ep)[2 * idx + 1];
+            const int sk = (rl >> 1) & 1;   // F16SWZ
+            const float4_t v0 = ((const float4_t*)ep)[2 * idx + sk];
+            const float4_t v1 = ((const float4_t*)ep)[2 * idx + (1 ^ sk)];
             if (row < M) {
               const half8_t h = {(_Float16)v0[0], (_Float16)v0[1], (_Float16)v0[2], (_Float16)v0[3],
                                  (_Float16)v1[0], (_Float16)v1[1], (_Float16)v1[2], (_Float16)v1[3]};

@@ -26,9 +26,13 @@ def main():
     ap.add_argument("--cfgs", default="81,82,83")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--w8-vitb", action="store_true", help="W8A8 vit_b shapes (int8 weights, EPI_Q8)")
+    ap.add_argument("--w8-vith", action="store_true",
+                    help="ViT-H W4A8 shapes and epilogues on int8-expanded weights (values in [-15, 15], BF_W8)")
     args = ap.parse_args()
     if args.w8_vitb:
         return w8_vitb(args)
+    if args.w8_vith:
+        return w8_vith(args)
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     cfgs = [int(c) for c in args.cfgs.split(",")]
@@ -70,6 +74,44 @@ def main():
                 print(f"{name:5s} M={m} cfg {c}: {best:8.1f} us  {fl / best / 1e6:7.1f} TOPS "
                       f"({fl / best / 1e6 / 5000 * 100:4.1f}% int8 peak)  identical to cfg 82: {same}", flush=True)
         print(f"M={m} per-block GEMM total: " + "  ".join(f"cfg {c} {t:.1f} us" for c, t in tot.items()), flush=True)
+
+
+def w8_vith(args):
+    """The ViT-H W4A8 shapes and epilogues with the int4 weights expanded to int8 (q - zp in [-15, 15]):
+    the int8 GEMM without any in-kernel unpack (BF_W8 kernels), timed like main()."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    cfgs = [int(c) for c in args.cfgs.split(",")]
+    for m in (int(x) for x in args.m.split(",")):
+        tot = {c: 0.0 for c in cfgs}
+        for name, (k, n, epi) in SHAPES.items():
+            w = torch.randint(-15, 16, (n, k), device=dev, dtype=torch.int8)
+            packed = ops.w8_repack(w)
+            ws = torch.rand(n, device=dev) * 0.01
+            bias = torch.randn(n, device=dev) * 0.02
+            a = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8)
+            osc = 0.05 if epi == ops.EPI_Q8_GELU else 0.0
+
+            def run(c, out):
+                return ops.i8_gemm(a, _lib.BF_W8, packed, ws, n, bias, None, epi, 0.02, osc, out=out, cfg=c)
+            stream = torch.cuda.current_stream()
+            for c in cfgs:
+                o = torch.zeros(m, n, device=dev, dtype=torch.float32) if epi == ops.EPI_RESADD_F32 else None
+                o = run(c, o)
+                best = 1e9
+                for _ in range(3):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    for _ in range(args.iters):
+                        run(c, o)
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    best = min(best, e0.elapsed_time(e1) / args.iters * 1e3)
+                tot[c] += best
+                fl = 2.0 * m * n * k
+                print(f"w8 {name:5s} M={m} cfg {c}: {best:8.1f} us  {fl / best / 1e6:7.1f} TOPS "
+                      f"({fl / best / 1e6 / 5000 * 100:4.1f}% int8 peak)", flush=True)
+        print(f"w8 M={m} per-block GEMM total: " + "  ".join(f"cfg {c} {t:.1f} us" for c, t in tot.items()), flush=True)
 
 
 def w8_vitb(args):
