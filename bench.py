@@ -57,8 +57,8 @@ def log(*a):
 
 
 # committed PMC passes (tools/pmc_all.sh) per (mode, GEMM rows per launch)
-PMC_PROFILES = {("w4a16", 16384): "r1_pmc_traffic_w4a16.json", ("w4a16", 8192): "r3_pmc_traffic_w4a16_m8192.json",
-                ("w4a8", 16384): "r3_pmc_traffic_w4a8_m16384.json", ("w8a8", 4096): "r3_pmc_traffic_w8a8_m4096.json"}
+PMC_PROFILES = {("w4a16", 16384): "r1_pmc_traffic_w4a16.json", ("w4a16", 8192): "r4_pmc_traffic_w4a16_m8192.json",
+                ("w4a8", 16384): "r4_pmc_traffic_w4a8_m16384.json", ("w8a8", 4096): "r4_pmc_traffic_w8a8_m4096.json"}
 
 
 def pmc_traffic(mode: str, profile: str):
