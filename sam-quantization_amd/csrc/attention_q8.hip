@@ -357,8 +357,39 @@ __device__ __forceinline__ void q8_rel_block(const AttnQ8Params& p, const int8_t
 //   O^T += V^T.P^T on 16x16x32 f16 MFMAs with P split hi + lo (|P - hi - lo| ~ 2^-22 |P|), V^T
 //       fragments by ds_read_b64_tr_b16 from the row-major fp16 V; the softmax denominators come
 //       from the same MFMAs against an all-ones operand (fp32 sums of the same hi + lo).
+// Softmax numerator table (round 4): the score codes are integers and the lazy offset m is one of
+// them, so P = exp2((c - m) k2) takes at most 256 + lazy distinct values, d = c - m in [-255, lazyc].
+// Entry 256 + d holds P split as fp16 hi (low half) + lo (high half) -- the operands the P.V MFMAs
+// take -- and entry 0 is P = 0 (a masked key: index max(int(-inf) + 256 - m, 0)), so a score costs
+// one LDS read and half a v_perm instead of fma + exp2 + three conversions + a subtraction.
+// P = exp2(fl(d k2)) (the table) vs exp2(fl(c k2 - fl(m k2))) (the direct form): last-bit
+// differences of fp32 P, below the 2^-22 of the hi + lo split.
+constexpr int PTAB = 512;
+__device__ __forceinline__ int q8_ptab_lazy(float k2) {   // lazy offset threshold in codes
+  return (int)fminf(floorf(8.0f / k2), 255.0f);
+}
+template <int NT>
+__device__ __forceinline__ void q8_ptab_fill(uint32_t* ptab, float k2, int lazyc, int tid) {
+  for (int i = tid; i <= 256 + lazyc; i += NT) {
+    const float pv = i == 0 ? 0.0f : __builtin_amdgcn_exp2f((float)(i - 256) * k2);
+    const _Float16 h = (_Float16)pv, l = (_Float16)(pv - (float)h);
+    ptab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+  }
+}
+// P^T fragments (hi, lo) of 8 scores from their table words (v_perm: two per pair of scores)
+__device__ __forceinline__ void q8_ptab_unpack(const uint32_t (&w)[8], half8_t& bhi, half8_t& blo) {
+  uint32_t hi[4], lo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x05040100u);
+    lo[j] = __builtin_amdgcn_perm(w[2 * j + 1], w[2 * j], 0x07060302u);
+  }
+  bhi = __builtin_bit_cast(half8_t, hi);
+  blo = __builtin_bit_cast(half8_t, lo);
+}
+
 template <int NWQ>
-__global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8Params p) {
+__global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(AttnQ8Params p) {
   constexpr int G = 64, KC = 64, VP = QD + 8;    // V row pitch (halves): spreads the tr reads over banks
   constexpr int NT = 64 * NWQ;
   constexpr int UNITS = KC * 4;                  // 16-byte pieces of one chunk's K (and of its V)
@@ -368,6 +399,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   __shared__ __attribute__((aligned(16))) _Float16 v_lds[2][KC * VP];
   __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
   __shared__ float rh_lds[NWQ][16 * (G + 1)];
+  __shared__ uint32_t ptab[PTAB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -378,6 +410,8 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   const int head = blockIdx.y;
   const int b = blockIdx.x;
   const int qy = blockIdx.z;                    // query grid row of this workgroup
+  const int lazyc = q8_ptab_lazy(p.k2);
+  q8_ptab_fill<NT>(ptab, p.k2, lazyc, tid);     // visible after the first barrier below
   const int qx = wave * 16 + ql;
   const int64_t ts = 3 * (int64_t)C;
   const int8_t* img = p.qkv + (int64_t)b * G * G * ts;
@@ -443,12 +477,14 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
   for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) rwr[bb][i] *= inv2;
-  // lazy softmax offset: m moves only when a code exceeds it by more than 8 / k2 (P <= 2^8, far
-  // inside fp16; O and l carry the same offset) -- most chunks then skip the O / l rescale
-  const float lazy = 8.0f / k2;
+  // lazy softmax offset: m moves only when a code exceeds it by more than lazyc = 8 / k2 codes
+  // (P <= 2^8, far inside fp16; O and l carry the same offset) -- most chunks then skip the O / l
+  // rescale; P comes from the table (ptab, d = c - m <= lazyc)
+  const float lazy = (float)lazyc;
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
   float m = -INFINITY;
+  int pofs = 0;   // 256 - m: the table index of code c is c + pofs
   float4_t acc[QD / 16], lacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -487,20 +523,17 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_row64_kernel(AttnQ8
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       lacc = lacc * alpha;
       m = cmax;
+      pofs = 256 - (int)cmax;
     }
-    const float off = -m * k2;
-    // ---- P (hi + lo fp16) and O^T += V^T.P^T, l += ones.P^T, two 32-key steps
+    // ---- P (hi + lo fp16, from the table) and O^T += V^T.P^T, l += ones.P^T, two 32-key steps
+    uint32_t pw[2][8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pw[j >> 3][j & 7] = ptab[(int)c[j >> 2][j & 3] + pofs];
     const _Float16* vb = &v_lds[buf][0];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       half8_t bhi, blo;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pv = __builtin_amdgcn_exp2f(fmaf(c[2 * s2 + (j >> 2)][j & 3], k2, off));
-        const _Float16 h = (_Float16)pv;
-        bhi[j] = h;
-        blo[j] = (_Float16)(pv - (float)h);
-      }
+      q8_ptab_unpack(pw[s2], bhi, blo);
 #pragma unroll
       for (int t = 0; t < QD / 16; ++t) {
         const _Float16* a0 = vb + (32 * s2 + 4 * g + trow) * VP + t * 16 + tcol;
@@ -630,13 +663,20 @@ __global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_wi
       if (4 * g + i < SW) rh_lds[wave][ql * (SW + 1) + 4 * g + i] = rh4[i];
     }
   }
-  __syncthreads();   // K / V staged; this wave's rel_h rows visible
+  __syncthreads();   // K / V staged; this wave's rel_h rows visible; q_lds read for the last time
+  // the P table (q8_ptab_fill) in q_lds's bytes: the two workgroups per CU leave no room for it
+  static_assert(sizeof(q_lds) >= PTAB * 4, "P table alias");
+  uint32_t* ptab = (uint32_t*)&q_lds[0][0];
+  const int lazyc = q8_ptab_lazy(p.k2);
+  q8_ptab_fill<64 * SW>(ptab, p.k2, lazyc, tid);
+  __syncthreads();
   const float* rhq = &rh_lds[wave][ql * (SW + 1)];
 
   const float c1 = p.qk_scale * p.inv_a1, inv2 = p.inv_a2, k2 = p.k2, k12 = p.s_a1 * p.inv_a2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) rwr[i] *= inv2;   // see the row64 kernel
-  const float lazy = 8.0f / k2;
+  const float lazy = (float)lazyc;
+  int pofs = 0;   // 256 - m (see the row64 kernel)
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
   float m = -INFINITY;
@@ -684,21 +724,20 @@ __global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_wi
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       lacc = lacc * alpha;
       m = cmax;
+      pofs = 256 - (int)cmax;
     }
-    const float off = -m * k2;
     const _Float16* vb = &v_lds[(ch * 64) * VP];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       if (2 * s2 >= nb) continue;   // both key rows of this k32 step are past the window
       half8_t bhi, blo;
+      uint32_t pw[8];   // masked keys (c = -inf): entry 0, P = 0
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float cv = c[2 * s2 + (j >> 2)][j & 3];
-        const float pv = cv == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(fmaf(cv, k2, off));
-        const _Float16 h = (_Float16)pv;
-        bhi[j] = h;
-        blo[j] = (_Float16)(pv - (float)h);
+        pw[j] = ptab[cv == -INFINITY ? 0 : (int)cv + pofs];
       }
+      q8_ptab_unpack(pw, bhi, blo);
 #pragma unroll
       for (int t = 0; t < QD / 16; ++t) {
         const _Float16* a0 = vb + (32 * s2 + 4 * g + trow) * VP + t * 16 + tcol;
