@@ -13,7 +13,9 @@
  *     thread-local message.  The Python layer maps SAMQ_ERR_INVALID -> AssertionError
  *     (the reference's shape asserts, quant_linear.py:378-399), SAMQ_ERR_UNSUPPORTED ->
  *     NotImplementedError (quant_linear.py:72-73, fused_attention.py:134-135) and
- *     SAMQ_ERR_HIP -> RuntimeError.
+ *     SAMQ_ERR_HIP -> RuntimeError;
+ *   - an empty batch (zero rows / tokens / images: M, rows, n or B == 0) returns 0 before any
+ *     pointer is checked or dereferenced (an empty tensor's data pointer may be null).
  * Data types: "f16" = IEEE binary16, "f32" = binary32; int4 weights use the reference's
  * GPTQ packing (qweight int32 (K/8,N), qzeros int32 (G,N/8), scales f16 (G,N),
  * gptq4sam.py:434-497) -- repacked once per layer by samq_w4_repack.

@@ -1595,6 +1595,7 @@ using namespace samq;
 static int rel_attention_impl(const void* qkv, const void* qkv_bias, const void* rel_pos_h, const void* rel_pos_w,
                               void* out, int B, int H, int W, int heads, int hd, int window, float sm_scale,
                               float out_scale, hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention: null pointer");
   SAMQ_REQUIRE(hd == 64 || hd == 80, SAMQ_ERR_UNSUPPORTED, "rel_attention: head_dim must be 64 or 80");
   SAMQ_REQUIRE(B > 0 && H > 0 && W > 0 && heads > 0, SAMQ_ERR_INVALID, "rel_attention: bad shape");

@@ -777,6 +777,7 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
                                      const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
                                      int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
                                      hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention_q8: null pointer");
   SAMQ_REQUIRE(hd == QD, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: head_dim must be 64");
   SAMQ_REQUIRE(B > 0 && H > 0 && W > 0 && heads > 0, SAMQ_ERR_INVALID, "rel_attention_q8: bad shape");

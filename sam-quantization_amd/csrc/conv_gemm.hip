@@ -447,6 +447,7 @@ using namespace samq;
 
 extern "C" int samq_patch_embed(const void* img, const void* weight, const float* bias, const float* pos, float* out,
                                 int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(img && weight && out, SAMQ_ERR_INVALID, "patch_embed: null pointer");
   SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
                "patch_embed: image size must be a multiple of the patch size");
@@ -462,6 +463,7 @@ extern "C" int samq_patch_embed(const void* img, const void* weight, const float
 
 extern "C" int samq_conv1x1_f32(const float* x, const void* weight, void* out, int64_t M, int N, int K,
                                 hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && weight && out, SAMQ_ERR_INVALID, "conv1x1: null pointer");
   SAMQ_REQUIRE(M > 0 && M < (int64_t)1 << 31, SAMQ_ERR_INVALID, "conv1x1: bad M");
   SAMQ_REQUIRE(K % 32 == 0 && N % 128 == 0, SAMQ_ERR_UNSUPPORTED,
@@ -474,6 +476,7 @@ extern "C" int samq_conv1x1_f32(const float* x, const void* weight, void* out, i
 
 extern "C" int samq_conv3x3_nhwc(const void* x, const void* weight, void* out, int B, int G, int Cin, int N,
                                  hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && weight && out, SAMQ_ERR_INVALID, "conv3x3: null pointer");
   SAMQ_REQUIRE(B > 0 && G > 0, SAMQ_ERR_INVALID, "conv3x3: bad shape");
   SAMQ_REQUIRE(Cin % 32 == 0 && N % 128 == 0, SAMQ_ERR_UNSUPPORTED,
@@ -486,6 +489,7 @@ extern "C" int samq_conv3x3_nhwc(const void* x, const void* weight, void* out, i
 
 extern "C" int samq_patch_embed_f32(const float* img, const float* weight, const float* bias, const float* pos,
                                     float* out, int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(img && weight && out, SAMQ_ERR_INVALID, "patch_embed_f32: null pointer");
   SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
                "patch_embed_f32: image size must be a multiple of the patch size");
@@ -508,6 +512,7 @@ extern "C" int samq_patch_embed_f32(const float* img, const float* weight, const
 extern "C" int samq_patch_embed_u8(const uint8_t* img, int h, int w, const float* pixel_mean, const float* pixel_std,
                                    const void* weight, int weight_f32, const float* bias, const float* pos, float* out,
                                    int B, int Cin, int img_size, int patch, int N, hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(img && pixel_mean && pixel_std && weight && out, SAMQ_ERR_INVALID, "patch_embed_u8: null pointer");
   SAMQ_REQUIRE(B > 0 && Cin > 0 && patch > 0 && img_size % patch == 0, SAMQ_ERR_INVALID,
                "patch_embed_u8: image size must be a multiple of the patch size");

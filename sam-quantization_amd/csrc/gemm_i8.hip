@@ -877,6 +877,7 @@ extern "C" int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const vo
                                 const int32_t* qzeros, const float* bias, void* C, int64_t ldc, const int8_t* R,
                                 int64_t ldr, int M, int N, int K, int epilogue, float a_scale, float mid_scale,
                                 float res_scale, float out_scale, int cfg, hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(A && wpacked && wscale && C, SAMQ_ERR_INVALID, "i8_gemm: null pointer");
   SAMQ_REQUIRE(bfmt == BF_W8 || bfmt == BF_W4, SAMQ_ERR_INVALID, "i8_gemm: unknown weight format");
   SAMQ_REQUIRE(bfmt == BF_W8 || qzeros, SAMQ_ERR_INVALID, "i8_gemm: W4 needs qzeros");
@@ -903,6 +904,7 @@ extern "C" int samq_w8a8_conv_gemm(const int8_t* x, int mode, int B, int Cin, in
                                    const float* wscale, const float* bias, void* C, const int8_t* R, int rmod,
                                    int N, int epilogue, float a_scale, float mid_scale, float res_scale,
                                    float out_scale, hipStream_t stream) {
+  if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && wpacked && wscale && C, SAMQ_ERR_INVALID, "w8a8_conv_gemm: null pointer");
   SAMQ_REQUIRE(mode == AG_PATCH || mode == AG_3X3, SAMQ_ERR_INVALID, "w8a8_conv_gemm: mode must be 1 (patch) or 2 (3x3)");
   SAMQ_REQUIRE(epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_RES, SAMQ_ERR_UNSUPPORTED,
@@ -951,6 +953,7 @@ extern "C" int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* w
     return samq_i8_gemm_cfg(A, lda, BF_W4, wpacked, wscale, qzeros, bias, C, ldc, nullptr, 0, M, N, K, epilogue,
                             a_scale, 0.f, 0.f, out_scale, cfg, stream);
   // grouped weights (gptq_triton/quant_linear.py:324-335: per-group scale / zero rows)
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(A && wpacked && wscale && qzeros && C, SAMQ_ERR_INVALID, "w4a8_gemm: null pointer");
   SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 128 == 0 && N % 64 == 0, SAMQ_ERR_INVALID,
                "w4a8_gemm: K % 128 == 0 and N % 64 == 0 required");

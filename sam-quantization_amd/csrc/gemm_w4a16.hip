@@ -2145,6 +2145,7 @@ extern "C" int samq_w4_repack(const int32_t* qweight, int32_t* packed, int K, in
 extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
                                    const int32_t* qzeros, const void* bias, void* C, int64_t ldc, int M, int N,
                                    int K, int groupsize, int epilogue, int cfg, hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(A && wpacked && scales && qzeros && C, SAMQ_ERR_INVALID, "w4a16_gemm: null pointer");
   SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0, SAMQ_ERR_INVALID, "w4a16_gemm: bad shape");
   SAMQ_REQUIRE(K % 64 == 0, SAMQ_ERR_INVALID, "w4a16_gemm: K must be a multiple of 64");
@@ -2180,6 +2181,7 @@ extern "C" int samq_w4a16_gemm_cfg(const void* A, int64_t lda, const int32_t* wp
 extern "C" int samq_w4a16_gated_mlp(const void* A, int64_t lda, const int32_t* wpacked, const void* scales,
                                     const int32_t* qzeros, void* C, int64_t ldc, int M, int N2, int K, int groupsize,
                                     hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(A && wpacked && scales && qzeros && C, SAMQ_ERR_INVALID, "w4a16_gated_mlp: null pointer");
   SAMQ_REQUIRE(M >= 0 && N2 > 0 && K > 0 && K % 64 == 0, SAMQ_ERR_INVALID,
                "w4a16_gated_mlp: K must be a positive multiple of 64");
@@ -2200,6 +2202,7 @@ extern "C" int samq_w4a16_gemm_lnf(const void* A, int64_t lda, const int32_t* wp
                                    int K, int groupsize, int epilogue, int cfg, const float* gamma, const float* gw,
                                    const float* bw, float* stats, float* mu, void* aout, float eps,
                                    hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(A && wpacked && scales && qzeros && C && stats && mu, SAMQ_ERR_INVALID, "w4a16_gemm_lnf: null pointer");
   SAMQ_REQUIRE(M >= 0 && N > 0 && K > 0 && K % 64 == 0 && N % 256 == 0, SAMQ_ERR_INVALID,
                "w4a16_gemm_lnf: K % 64 == 0 and N % 256 == 0 required");

@@ -150,6 +150,7 @@ static int ln_rpw(int flags) {
 static int ln_launch(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C, float eps,
                      int in, int out, float in_scale, float out_scale, int rpw, hipStream_t stream,
                      float* mean_out = nullptr) {
+  if (rows == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && y && gamma && beta, SAMQ_ERR_INVALID, "layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 4096, SAMQ_ERR_INVALID, "layernorm: C must be a multiple of 4, <= 4096");
   if (rows <= 0) return SAMQ_OK;
@@ -202,6 +203,7 @@ extern "C" int samq_layernorm_mean(const void* x, void* y, const float* gamma, c
 // moved out of its epilogue.  Rows of C <= 1280 (the ViT-H / vit_b widths).
 extern "C" int samq_add_layernorm(void* x, const void* delta, void* y, const float* gamma, const float* beta,
                                   int64_t rows, int C, float eps, int flags, float out_scale, hipStream_t stream) {
+  if (rows == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && delta && y && gamma && beta, SAMQ_ERR_INVALID, "add_layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 1280, SAMQ_ERR_INVALID, "add_layernorm: C must be a multiple of 4, <= 1280");
   SAMQ_REQUIRE(!(flags & SAMQ_LN_OUT_I8) || out_scale > 0.f, SAMQ_ERR_INVALID, "add_layernorm: out_scale must be > 0");

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void quantize_kernel(const void* __restrict__ 
 using namespace samq;
 
 extern "C" int samq_quantize(const void* x, void* y, int64_t n, float scale, int flags, hipStream_t stream) {
+  if (n == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && y, SAMQ_ERR_INVALID, "quantize: null pointer");
   SAMQ_REQUIRE(scale > 0.f, SAMQ_ERR_INVALID, "quantize: scale must be > 0");
   SAMQ_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0, SAMQ_ERR_INVALID,
@@ -92,6 +93,7 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(const float* __restrict__
 }  // namespace samq
 
 extern "C" int samq_silu_mul(const float* gate, const float* up, void* out, int64_t n, hipStream_t stream) {
+  if (n == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(gate && up && out, SAMQ_ERR_INVALID, "silu_mul: null pointer");
   if (n <= 0) return SAMQ_OK;
   const int blocks = (int)((n + 255) / 256 < 16384 ? (n + 255) / 256 : 16384);

@@ -577,3 +577,44 @@ def test_w4a16_gemm_lnf_consumer_k_limit(cuda, groupsize, cfg, k, ok):
     else:
         with pytest.raises(NotImplementedError):
             lin.forward_lnf(a, ops.EPI_BIAS_LNF, out, stats, mu, gw=gw, bw=bw, eps=1e-6)
+
+
+@pytest.mark.gpu
+def test_empty_batch_inputs(cuda):
+    """Zero rows / zero images through every product entry point of the hot path (the engines'
+    batch can be split into an empty shard on a rank): no launch fault, empty outputs of the right
+    shape, and a following non-empty call still correct."""
+    from samq import ops
+    k, n = 256, 256
+    qw, qz, sc, bias = _packed_layer(k, n, -1, seed=3)
+    packed = ops.w4_repack(_dev(qw, cuda))
+    args = (packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, -1)
+    a0 = torch.zeros((0, k), dtype=torch.float16, device=cuda)
+    assert ops.w4a16_gemm(a0, *args, ops.EPI_BIAS).shape == (0, n)
+    assert ops.w4a16_gemm(a0, *args, ops.EPI_BIAS_GELU).shape == (0, n)
+    r0 = torch.zeros((0, n), dtype=torch.float32, device=cuda)
+    ops.w4a16_gemm(a0, *args, ops.EPI_RESADD_F32, out=r0)
+    # int8 paths
+    w8 = torch.randint(-127, 128, (n, k), dtype=torch.int8, device=cuda)
+    p8 = ops.w8_repack(w8)
+    ws = torch.rand(n, device=cuda) * 0.01
+    b32 = torch.zeros(n, device=cuda)
+    a8 = torch.zeros((0, k), dtype=torch.int8, device=cuda)
+    assert ops.w8a8_gemm(a8, p8, ws, n, b32, ops.EPI_Q8, 0.02, 0.05).shape == (0, n)
+    assert ops.quantize(torch.zeros(0, device=cuda), 0.1).numel() == 0
+    x0 = torch.zeros((0, 1280), dtype=torch.float32, device=cuda)
+    g = torch.ones(1280, device=cuda)
+    assert ops.layernorm(x0, g, torch.zeros(1280, device=cuda)).shape == (0, 1280)
+    # attention over zero images (windowed and global)
+    qkv0 = torch.zeros((0, 64, 64, 3 * 1280), dtype=torch.float16, device=cuda)
+    rh = torch.zeros((127, 80), dtype=torch.float16, device=cuda)
+    rw = torch.zeros((27, 80), dtype=torch.float16, device=cuda)
+    assert ops.rel_attention(qkv0, None, rh, rh, 16, 0, 80 ** -0.5).shape == (0, 64, 64, 1280)
+    assert ops.rel_attention(qkv0, None, rw, rw, 16, 14, 80 ** -0.5).shape == (0, 64, 64, 1280)
+    torch.cuda.synchronize()
+    # a normal call afterwards
+    m = 300
+    rng = np.random.Generator(np.random.PCG64(4))
+    a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
+    y = gptq_pack.matmul4_g1(a, qw, sc, qz, -1, bias)
+    _close(ops.w4a16_gemm(_dev(a, cuda), *args, ops.EPI_BIAS), y, 2e-3)

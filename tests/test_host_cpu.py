@@ -41,6 +41,22 @@ def test_c_abi_rejects_bad_shapes_before_touching_the_device():
         _lib.check(st)
 
 
+def test_c_abi_empty_batch_is_a_no_op():
+    """An empty batch (M / rows / n / B == 0) returns SAMQ_OK before any pointer is checked or a
+    launch is made (an empty tensor's data pointer is null), while a negative size is still an
+    error -- runs without a GPU since nothing reaches the device (include/samq.h conventions)."""
+    from samq import _lib
+    lib = _lib.load()
+    assert lib.samq_w4a16_gemm(None, 1280, None, None, None, None, None, 3840, 0, 3840, 1280, -1, 0, None) == 0
+    assert lib.samq_w4a16_gemm(None, 1280, None, None, None, None, None, 3840, -1, 3840, 1280, -1, 0,
+                               None) == _lib.SAMQ_ERR_INVALID
+    assert lib.samq_layernorm(None, None, None, None, 0, 1280, 1e-6, 0, None) == 0
+    assert lib.samq_quantize(None, None, 0, 0.1, 0, None) == 0
+    assert lib.samq_rel_attention(None, None, None, None, None, 0, 64, 64, 16, 80, 14, 0.1, None) == 0
+    assert lib.samq_rel_attention(None, None, None, None, None, 1, 64, 64, 16, 80, 14, 0.1,
+                                  None) == _lib.SAMQ_ERR_INVALID
+
+
 def test_c_abi_rejects_timing_and_layout2_configs():
     """The product library exposes only tile configs that compute the GEMM on layout-1 weights:
     the tuning build's timing-only variants (27/28 no unpack, 70-73 no MFMA / no restaging) and the
