@@ -882,12 +882,14 @@ __global__ __launch_bounds__(256, 2) void win_attention_kernel(AttnParams p, int
 //    score registers' order, which IS the B operand of O^T += V^T . P^T (k-slot 8h + j <-> key
 //    16u + 4h + j (j < 4) / 16u + 8 + 4h + j - 4);
 //  * V^T fragments by ds_read_b64_tr_b16 from 4-key x 32-dim chunks (256 contiguous bytes per
-//    read group: conflict-free); d-block 2 covers dims 64..95, its rows 80..95 forced to 1.0 so
-//    the same MFMAs produce the softmax row sums (no extra MFMA, no VALU sum);
+//    read group: conflict-free); d-block 2 covers dims 64..95, its rows 80..95 read as 1.0 (a
+//    ones region per ring slot, ONESL below) so the same MFMAs produce the softmax row sums (no
+//    extra MFMA, no VALU sum);
 //  * K pieces lane-linear (lane l of piece (kt, s) = key 32 kt + l % 32, dims 16 s + 8 (l / 32):
-//    the A fragment read is ds_read_b128 at l * 16); key rows stream through a 3-deep LDS ring
-//    (20 KiB per row, LDS-DMA, 20 pieces over 8 waves), one barrier per key row, the next row's
-//    Q.K^T MFMAs issued ahead of the current row's softmax.
+//    the A fragment read is ds_read_b128 at l * 16); key rows stream through a 5-slot LDS ring
+//    (20 KiB of K / V per row, LDS-DMA, 20 pieces over 8 waves), two barriers per key row (the
+//    two-group ping-pong below), the next row's Q.K^T MFMAs issued ahead of the current row's
+//    softmax.
 __device__ __forceinline__ float16_t mfma32(half8_t a, half8_t b, float16_t c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
@@ -1061,7 +1063,7 @@ __global__ __launch_bounds__(512, 1) void glob80_attention_kernel(AttnParams p) 
 
   // ---- V^T fragment addresses (ds_read_b64_tr_b16): lane 4q + p of its 16-lane group reads
   // key 4 kq + q, dims 16 g16 + 4p .. of the chunk; d-block 2 lanes g16 = 1 (dims 80..95) read
-  // the g16 = 0 bytes and are forced to 1.0 below
+  // the slot's ones (ONESL; the round-3 layout read the g16 = 0 bytes and forced 1.0 in pv)
   const int i16 = lane & 15, g16 = (lane >> 4) & 1;
   const int tq = i16 >> 2, tp = i16 & 3;
   constexpr int QB = ONESL ? 512 : 640, QB2 = ONESL ? 128 : 640;   // bytes per key quad (dims 0..63 / 64..79)
