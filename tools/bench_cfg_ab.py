@@ -36,7 +36,12 @@ for name, cfg in VARIANTS.items():
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             getattr(p, lay).gemm_cfg = cfg.get(lay, 0)
+    envs = {k[4:]: str(v) for k, v in cfg.items() if k.startswith("env_")}   # tuning-build knobs, e.g.
+    for k, v in envs.items():                                                # "env_SAMQ_ATTN_WIN=8"
+        os.environ[k] = v
     graph, out = eng.capture(img, lanes=lanes)
+    for k in envs:
+        del os.environ[k]
     graph.replay()
     torch.cuda.synchronize()
     ref = out.clone() if ref is None else ref

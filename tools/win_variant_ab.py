@@ -26,10 +26,15 @@ args = (t(qkv16), t(bq), t(rph), t(rpw), 16, 14, 80 ** -0.5)
 s = float(np.abs(ref).max() / 100)
 codes = np.clip(np.rint(ref / np.float32(s)), -128, 127)
 times = {v: [] for v in variants}
+first = {}
 for v in variants:
     os.environ["SAMQ_ATTN_WIN"] = str(v)
     o16 = ops.rel_attention(*args).float().cpu().numpy()
     o8 = ops.rel_attention(*args, out_scale=s).cpu().numpy().astype(np.int32)
+    first.setdefault("o16", o16)
+    first.setdefault("o8", o8)
+    print(f"window variant {v}: identical to variant {variants[0]}: fp16 {np.array_equal(o16, first['o16'])}, "
+          f"int8 {np.array_equal(o8, first['o8'])}", flush=True)
     print(f"window variant {v}: fp16 out max-abs vs oracle {np.abs(o16 - ref).max():.3e}, int8 codes off by one "
           f"{float((o8 != codes).mean()):.2e} (max |d| {int(np.abs(o8 - codes).max())})", flush=True)
 out = torch.empty(qkv16.shape[:3] + (1280,), dtype=torch.float16, device=dev)
