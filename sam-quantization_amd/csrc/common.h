@@ -139,8 +139,18 @@ __device__ __forceinline__ float2_t q8_exact2(float2_t v, float s, float inv, fl
   return float2_t{__builtin_amdgcn_fmed3f(__builtin_rintf(q2.x), -128.f, 127.f),
                   __builtin_amdgcn_fmed3f(__builtin_rintf(q2.y), -128.f, 127.f)};
 }
-// four codes (integer floats in [-128, 127]) -> their int8 bytes in one dword: v_cvt_pk_u8_f32 of
-// code + 128 (exact integers in [0, 255]) per byte, then the sign bit flipped back per byte
+// round_half_even(v * fl(1/s)), NOT clamped: the quotient by one reciprocal multiply (<= 1.5 ulp from
+// v / s, so a code differs from the exact quotient's only within ~1e-7 of a rounding midpoint); the
+// clamp to [-128, 127] is q8_pack4's saturating conversion.  For the GELU epilogues only: the GELU in
+// front of it is itself an approximation (|error| 7.1e-7, gelu_r16_2), so the exact quotient of
+// q8_exact2 buys nothing there; 3 VALU per pair instead of 11.
+__device__ __forceinline__ float2_t q8_recip2(float2_t v, float inv) {
+  const float2_t q = v * (float2_t)(inv);
+  return float2_t{__builtin_rintf(q.x), __builtin_rintf(q.y)};
+}
+// four codes (integer floats) -> their int8 bytes in one dword: v_cvt_pk_u8_f32 of code + 128 per
+// byte, then the sign bit flipped back per byte.  The conversion saturates to [0, 255] (and rounds to
+// nearest even; gfx950, tools/probe_cvt_u8.hip), so codes outside [-128, 127] come out clamped
 __device__ __forceinline__ uint32_t q8_pack4(float c0, float c1, float c2, float c3) {
   uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(c0 + 128.f, 0, 0u);
   w = __builtin_amdgcn_cvt_pk_u8_f32(c1 + 128.f, 1, w);

@@ -1871,14 +1871,18 @@ static int launch_v4(const GemmArgs& a, hipStream_t st) {
   return SAMQ_OK;
 }
 
+// CU count of the CURRENT device, cached per device id (a process may drive several GPUs)
 static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
+  static int cached[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cached[dev] == 0) {
+    int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
   }
-  return n;
+  return cached[dev];
 }
 
 template <int WMW, int TM, int TN, int NPH, int STAGES, int LA, int EPI, int VAR = 0>
@@ -1891,7 +1895,10 @@ static int launch_pp2(const GemmArgs& a, hipStream_t st) {
     if (a.K > kmax) return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm_lnf: consumer K exceeds this config's LDS row-partial budget");
   }
   int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
-  if ((VAR & (1 << 20)) != 0 && nwg > cu_count()) nwg = cu_count() & ~7;   // persistent: <= 1 workgroup per CU
+  if ((VAR & (1 << 20)) != 0 && nwg > cu_count()) {   // persistent: <= 1 workgroup per CU, whole XCD rounds
+    const int cus = cu_count() & ~7;
+    nwg = cus >= 8 ? cus : cu_count();
+  }
   hipLaunchKernelGGL((w4a16_gemm_pp2<WMW, TM, TN, NPH, STAGES, LA, EPI, VAR>), dim3(nwg), dim3(512), 0, st,
                      a.A, a.lda, a.Wp, a.scales, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.groupsize / 64, a.lnf);
   SAMQ_LAUNCH_CHECK("w4a16_gemm_pp2 launch");
@@ -1946,7 +1953,8 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 107: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 20)>(a, st);
       // cfg 57 / 64 with the epilogue's scale / bias loaded before the prologue (VAR & (1 << 21))
       case 109: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 21)>(a, st);
-      // cfg 57 with the transposed f16 staging epilogue (f16 outputs; f32 outputs take cfg 57's)
+      // cfg 57 with the transposed f16 staging epilogue for f16 outputs; f32 outputs (RESADD_F32 /
+      // F32) have no f16 staging and run cfg 57 itself
       case 111:
         if constexpr (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | (1 << 22)>(a, st);
         else return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
@@ -1955,7 +1963,7 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       // cfg 57 with transposed accumulators and the f16-staged epilogue (f16 outputs only)
       case 104:
         if constexpr (EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU) return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 65536>(a, st);
-        else return fail(SAMQ_ERR_INVALID, "w4a16_gemm: cfg 104 has f16 epilogues (BIAS / BIAS_GELU) only");
+        else return fail(SAMQ_ERR_UNSUPPORTED, "w4a16_gemm: cfg 104 has f16 epilogues (BIAS / BIAS_GELU) only");
       case 101: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096 | 16384>(a, st);
 #ifdef SAMQ_TUNING
       // tuning build only (make tuning): untested shapes and TIMING-ONLY variants that compute

@@ -17,14 +17,17 @@ __device__ __forceinline__ float ln_q8(float v, float s) {   // fq_vit uniform.p
 // ADD (f32 input only): the residual add of the GEMM before the LayerNorm runs here instead of in
 // that GEMM's epilogue -- x += delta (delta f16 when ADD == 1, f32 when ADD == 2; the GEMM wrote
 // y = acc * s + b with a plain store), x written back in place, then the LayerNorm of the new x.
-// f32 delta: the same fp32 add as the GEMM's read-modify-write epilogue (bit-identical x).
+// f32 delta: the same fp32 add as the GEMM's read-modify-write epilogue (bit-identical x).  The ADD
+// variants read AND write the residual through ``xres`` (plain, non-const: the buffer is updated in
+// place); ``xin`` (const restrict) is the input of the ADD == 0 variants only.
 template <int IN, int OUT, int VPT, int RPW, int ADD = 0>
 __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__ xin, void* __restrict__ y,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, int64_t rows, int C,
                                                         float eps, float in_scale, float out_scale,
                                                         float* __restrict__ mean_out,
-                                                        const void* __restrict__ delta = nullptr) {
+                                                        const void* __restrict__ delta = nullptr,
+                                                        float* xres = nullptr) {
   static_assert(ADD == 0 || IN == LN_F32, "residual add: f32 rows");
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[r][i][e] = (float)(int8_t)((w >> (8 * e)) & 0xFFu) * in_scale;
         } else {
-          v[r][i] = ((const float4_t*)xin)[row * nvec + j];
+          v[r][i] = ADD != 0 ? ((const float4_t*)xres)[row * nvec + j] : ((const float4_t*)xin)[row * nvec + j];
           if constexpr (ADD == 1) {
             const half4_t h = ((const half4_t*)delta)[row * nvec + j];
             v[r][i] += float4_t{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
           const int j = lane + 64 * i;
-          if (j < nvec) ((float4_t*)xin)[row * nvec + j] = v[r][i];
+          if (j < nvec) ((float4_t*)xres)[row * nvec + j] = v[r][i];
         }
       }
     }
@@ -213,8 +216,9 @@ extern "C" int samq_add_layernorm(void* x, const void* delta, void* y, const flo
   const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
   const bool i8 = (flags & SAMQ_LN_OUT_I8) != 0, d16 = (flags & SAMQ_LN_DELTA_F16) != 0;
   const int vpt = (C / 4 + 63) / 64;
-#define ALN(O, V, R, A) hipLaunchKernelGGL((layernorm_kernel<LN_F32, O, V, R, A>), grid, dim3(256), 0, stream, x, y, gamma, \
-                                           beta, rows, C, eps, 1.f, out_scale, nullptr, delta)
+#define ALN(O, V, R, A) hipLaunchKernelGGL((layernorm_kernel<LN_F32, O, V, R, A>), grid, dim3(256), 0, stream, \
+                                           (const void*)nullptr, y, gamma, beta, rows, C, eps, 1.f, out_scale, nullptr, \
+                                           delta, (float*)x)
 #define ALN_R(O, V, A) do { if (rpw == 1) ALN(O, V, 1, A); else if (rpw == 2) ALN(O, V, 2, A); else ALN(O, V, 4, A); } while (0)
 #define ALN_V(O, A) do { if (vpt <= 3) ALN_R(O, 3, A); else if (vpt <= 4) ALN_R(O, 4, A); else ALN_R(O, 5, A); } while (0)
   if (i8) { if (d16) ALN_V(LN_I8, 1); else ALN_V(LN_I8, 2); }

@@ -103,10 +103,18 @@ def _epi_check(ops, cuda, a, y, packed, sc, qz, bias, n, groupsize, epi, cfg, rn
 def test_w4a16_gemm_pingpong(cuda, cfg, epi):
     """v6 ping-pong kernels (256-row tiles, 2 staggered wave groups, 3/4-slot LDS-DMA rings):
     ragged M, short and long K (1 .. 40 K tiles, so the ring prologue / retire paths all run).
-    cfg 104 (transposed accumulators, f16-staged epilogue) has the f16 epilogues only."""
+    cfg 104 (transposed accumulators, f16-staged epilogue) has the f16 epilogues only and refuses
+    the f32 ones with NotImplementedError (SAMQ_ERR_UNSUPPORTED)."""
     from samq import ops
     if cfg == 104 and epi in ("resadd", "f32"):
-        pytest.skip("cfg 104: f16 epilogues only")
+        qw, qz, sc, bias = _packed_layer(256, 256, -1, seed=104)
+        a = torch.zeros((256, 256), dtype=torch.float16, device=cuda)
+        e = ops.EPI_RESADD_F32 if epi == "resadd" else ops.EPI_F32
+        out = torch.zeros((256, 256), dtype=torch.float32, device=cuda)
+        with pytest.raises(NotImplementedError):
+            ops.w4a16_gemm(a, ops.w4_repack(_dev(qw, cuda)), _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), 256,
+                           -1, e, out=out, cfg=104)
+        return
     for m, k, n in ((333, 1280, 512), (300, 64, 256), (260, 192, 256), (513, 2560, 768)):
         qw, qz, sc, bias = _packed_layer(k, n, -1, seed=cfg * 13 + k)
         rng = np.random.Generator(np.random.PCG64(cfg + k))

@@ -239,3 +239,17 @@ def test_bench_oracle_state_matches_test_oracle():
     a = sam_ref.EncoderOracle(cfg, st2, linear_weights=lw, linear_bias=lb)(img).numpy()
     b = oracle_g1(cfg, st, names, q)(img).numpy()
     np.testing.assert_array_equal(a, b)
+
+
+def test_bench_parity_report_cpu():
+    """bench.parity_report (the BENCH line's parity stanza): max-abs vs the oracle and the mask IoU
+    of the decoder run on both embeddings -- identical embeddings give IoU 1, a sign-flipped one
+    does not."""
+    import bench
+    g = torch.Generator().manual_seed(0)
+    ref = torch.randn((1, 256, 64, 64), generator=g) * 0.5
+    rec = bench.parity_report("w4a16", ref.clone(), ref)
+    assert rec["max_abs_vs_oracle"] == 0.0 and rec["pass"] is True
+    assert rec["mask_iou_min"] == 1.0 and rec["masks"] == 20
+    bad = bench.parity_report("w8a8", -ref, ref)
+    assert bad["pass"] is False and bad["cosine"] < -0.99 and bad["mask_iou_min"] < 0.9

@@ -118,7 +118,7 @@ def test_w8a8_gemm_epilogues(cuda, cfg):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 85, 86])
+@pytest.mark.parametrize("cfg", [0, 81, 82, 83, 85, 86, 93])
 def test_w4a8_gemm_exact_integer(cuda, cfg):
     """int4 (layout 3, incl. a zero point of 0 -> quirk 4) x int8: integer sums are exact."""
     from oracle import gptq_pack
@@ -202,10 +202,10 @@ def test_w4a8_gemm_grouped(cuda, groupsize, k, cfg):
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,n", [(300, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280), (77, 128, 256),
                                    (260, 256, 768)])
-@pytest.mark.parametrize("cfg", [85, 86])
+@pytest.mark.parametrize("cfg", [85, 86, 93])
 def test_w4a8_pingpong_matches_v3(cuda, m, k, n, cfg):
     """The W4A8 ping-pong kernels (cfg 85; cfg 86 = zero point applied through per-row sums of the
-    int8 activations) against the v3-style 256x256 kernel (cfg 81): all sum the same int32 products
+    int8 activations; cfg 93 = cfg 86 with the LDS-DMA pieces spread through the MFMA bursts) against the v3-style 256x256 kernel (cfg 81): all sum the same int32 products
     exactly and share the epilogue code, so every epilogue must agree BIT FOR BIT -- ragged M,
     K = 128 (one K tile, shorter than the lookahead), K = 256 (= the lookahead), and the lin2 depth
     K = 5120.  The weights include zero points of 0..15 (nibble + 1 = 1..16) and saturated codes."""

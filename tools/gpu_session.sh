@@ -1,45 +1,87 @@
 #!/bin/bash
-# One GPU-box session: each GPU step under its own time limit; a crash / abort / timeout
-# (exit status other than 0 = pass or 1 = test failures) stops the session immediately.
-# usage: tools/gpu_session.sh <step> [<step> ...]   steps: kernels encoder gpu bench smoke instep prof
+# One GPU-box session (the single runner for every gpurun call): each GPU step under its own time
+# limit; a crash / abort / timeout (exit status other than 0 = pass or 1 = test failures) stops
+# the session immediately, and no step is retried.
+# usage: tools/gpu_session.sh <tag> <step> [<step> ...]       logs: gpurun_out/<tag>.<step>.log
+# steps:
+#   gpu                    whole GPU suite (-s -rA: the [parity] lines are kept)
+#   kernels|w8a8|w4a8|encoder|decoder   one GPU test file
+#   k=<pytest -k expr>     GPU tests selected by -k
+#   smoke                  __graft_entry__.smoke()
+#   bench | bench48 | bench88 | benchg       full bench lines (w4a16 / w4a8 / w8a8 / G=128)
+#   benchq | b48q | b88q   bench lines without CPU baseline
+#   instep | instep48 | instep88 | instepg   rocprofv3 in-step kernel traces (tools/instep_profile.sh)
+#   pmc                    PMC HBM traffic of every mode (tools/pmc_all.sh)
+#   attnpmc                attention counters (tools/attn_pmc.sh)
+#   pmci8                  int8 GEMM counters (tools/pmc_i8.sh)
+#   i8=<cfgs>@<m>          int8 GEMM tile configs (tools/bench_i8.py, tuning library)
+#   w4=<cfgs>@<m>          W4A16 GEMM tile configs (tools/bench_gemm.py, tuning library)
+#   ab48=<variants>        in-graph W4A8 per-layer cfg A/B (tools/bench_cfg_ab_w4a8.py, tuning library)
+#   ab16=<variants>        in-graph W4A16 per-layer cfg A/B (tools/bench_cfg_ab.py, tuning library)
+#   abl=<mode>@<lib.so>    bench <mode> alternating this build and <lib.so> (SAMQ_LIB), 2 rounds each
+#   attn                   attention kernels isolated (tools/bench_attn.py)
+#   probe                  v_cvt_pk_u8_f32 semantics (tools/probe_cvt_u8.hip, built on the box)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+tag=${1:?tag}
+shift
 run() {  # name, seconds, command...
   local name=$1 secs=$2; shift 2
-  echo "=== [$name] $(date +%T) start" | tee -a gpurun_out/session.log
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local log="gpurun_out/$tag.$name.log"
+  echo "=== [$name] $(date +%T) start" | tee -a "gpurun_out/$tag.session.log"
+  timeout -k 10 "$secs" "$@" > "$log" 2>&1
   local rc=$?
-  echo "=== [$name] $(date +%T) rc=$rc" | tee -a gpurun_out/session.log
-  tail -n 25 "gpurun_out/$name.log"
+  echo "=== [$name] $(date +%T) rc=$rc" | tee -a "gpurun_out/$tag.session.log"
+  tail -n 25 "$log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
-    echo "=== stopping session after rc=$rc" | tee -a gpurun_out/session.log
+    echo "=== stopping session after rc=$rc" | tee -a "gpurun_out/$tag.session.log"
     exit $rc
   fi
 }
+PYT="python -u -m pytest -x --timeout 200 --timeout-method thread -m gpu -s -rA"
 for step in "$@"; do
+  arg=${step#*=}
   case $step in
-    kernels) run kernels 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rA ;;
-    w8a8)    run w8a8 600 python -m pytest tests/test_w8a8.py -q -m gpu -s -rA ;;
-    w4a8)    run w4a8 600 python -m pytest tests/test_w4a8.py -q -m gpu -s -rA ;;
-    encoder) run encoder 700 python -m pytest tests/test_gpu_encoder.py -q -m gpu -s -rA ;;
-    gpu)     run gputests 900 python -m pytest tests -q -m gpu -s -rA ;;
-    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench)   run bench 500 python bench.py --steps 20 --warmup 5 ;;
-    bench48) run bench_w4a8 600 python bench.py --mode w4a8 --steps 10 --warmup 3 ;;
-    bench88) run bench_w8a8 600 python bench.py --mode w8a8 --steps 20 --warmup 5 ;;
-    b48q)    run b48q 400 python bench.py --mode w4a8 --steps 10 --warmup 3 --no-cpu-baseline ;;
-    b88q)    run b88q 400 python bench.py --mode w8a8 --steps 20 --warmup 5 --no-cpu-baseline ;;
-    benchq)  run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
-    instep)  run instep 500 bash tools/instep_profile.sh w4a16 ;;
-    benchg)  run benchg 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --groupsize 128 ;;
-    instepg) run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128 ;;
-    grouped) run grouped 600 python -m pytest tests/test_gpu_kernels.py -q -m gpu -rA -k "grouped or auto_pick or configs" ;;
+    gpu)      run gputests 1100 $PYT -q tests ;;
+    kernels)  run kernels 600 $PYT -q tests/test_gpu_kernels.py ;;
+    w8a8)     run w8a8 600 $PYT -q tests/test_w8a8.py ;;
+    w4a8)     run w4a8 600 $PYT -q tests/test_w4a8.py ;;
+    encoder)  run encoder 700 $PYT -q tests/test_gpu_encoder.py ;;
+    decoder)  run decoder 600 $PYT -q tests/test_sam_decoder.py ;;
+    k=*)      run k_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 900 $PYT -q tests -k "$arg" ;;
+    smoke)    run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)    run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    bench48)  run bench48 600 python bench.py --mode w4a8 --steps 10 --warmup 3 ;;
+    bench88)  run bench88 600 python bench.py --mode w8a8 --steps 20 --warmup 5 ;;
+    benchg)   run benchg 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --groupsize 128 ;;
+    benchq)   run benchq 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    b48q)     run b48q 400 python bench.py --mode w4a8 --steps 10 --warmup 3 --no-cpu-baseline ;;
+    b88q)     run b88q 400 python bench.py --mode w8a8 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    instep)   run instep 500 bash tools/instep_profile.sh w4a16 ;;
     instep48) run instep48 500 bash tools/instep_profile.sh w4a8 ;;
-    instepb8) run instepb8 500 bash tools/instep_profile.sh w4a16 --batch 8 ;;
     instep88) run instep88 500 bash tools/instep_profile.sh w8a8 ;;
-    prof)    run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline ;;
+    instepg)  run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128 ;;
+    pmc)      run pmc 900 bash tools/pmc_all.sh ;;
+    attnpmc)  run attnpmc 400 bash tools/attn_pmc.sh ;;
+    pmci8)    run pmci8 400 bash tools/pmc_i8.sh ;;
+    i8=*)     run i8_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_i8.py \
+                --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 ;;
+    w4=*)     run w4_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_gemm.py \
+                --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 ;;
+    ab48=*)   run ab48 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab_w4a8.py 2 6 "$arg" ;;
+    ab16=*)   run ab16 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab.py 2 6 "$arg" ;;
+    abl=*)    m=${arg%@*}; lib=${arg#*@}
+              for r in 1 2; do
+                run abl_${m}_new_$r 400 python bench.py --mode "$m" --steps 10 --warmup 3 --no-cpu-baseline --no-isolated
+                run abl_${m}_lib_$r 400 env SAMQ_LIB="$lib" python bench.py --mode "$m" --steps 10 --warmup 3 --no-cpu-baseline --no-isolated
+              done
+              for f in gpurun_out/$tag.abl_${m}_*.log; do
+                echo "$f $(grep -h '"value"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+              done ;;
+    attn)     run attn 300 python -u tools/bench_attn.py ;;
+    probe)    run probe 120 bash -c "hipcc --offload-arch=gfx950 -O2 -o gpurun_out/probe_cvt_u8 tools/probe_cvt_u8.hip && gpurun_out/probe_cvt_u8" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -14,7 +14,7 @@ tag=$(echo "$*" | tr -c 'a-zA-Z0-9' '_')
 d=gpurun_out/instep_$mode$tag
 rm -rf "$d"
 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --stats -d "$d" -o run --output-format csv -- \
-  python3 bench.py --mode "$mode" --steps $steps --warmup 3 --no-cpu-baseline --no-isolated "$@" > "$d.log" 2>&1
+  python3 bench.py --mode "$mode" --steps $steps --warmup 3 --no-cpu-baseline --no-isolated --no-modes "$@" > "$d.log" 2>&1
 name=$(python3 - "$mode" "$d.log" <<'PY'
 import json, sys
 sys.path.insert(0, ".")
