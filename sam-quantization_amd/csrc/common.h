@@ -108,6 +108,40 @@ __device__ __forceinline__ float2_t gelu_r16_2(float2_t x) {
   return __builtin_elementwise_fma(-ax, r, m);
 }
 
+// gelu_r16_2 on N pairs at once, stage by stage across the pairs: the per-pair form is a chain of
+// ~12 dependent packed ops (Horner, four squarings, rcp), which at two waves per SIMD left the VALU
+// waiting on each result (the compiler padded the chains with s_nop); N independent chains in
+// lockstep fill those slots.  Same operations, same results as gelu_r16_2 per pair.
+template <int N>
+__device__ __forceinline__ void gelu_r16_n(float2_t (&x)[N]) {
+  float2_t ax[N], p[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    ax[n] = __builtin_elementwise_abs(x[n]);
+    p[n] = __builtin_elementwise_fma((float2_t)(5.6212996640e-06f), ax[n], (float2_t)(5.1055209009e-05f));
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], ax[n], (float2_t)(3.9686137011e-05f));
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], ax[n], (float2_t)(3.4227392389e-03f));
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], ax[n], (float2_t)(2.2076998457e-02f));
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], ax[n], (float2_t)(5.2075163037e-02f));
+#pragma unroll
+  for (int n = 0; n < N; ++n) p[n] = __builtin_elementwise_fma(p[n], ax[n], (float2_t)(1.0442737824e+00f));
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int n = 0; n < N; ++n) p[n] = p[n] * p[n];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const float2_t r = {__builtin_amdgcn_rcpf(p[n].x), __builtin_amdgcn_rcpf(p[n].y)};
+    const float2_t m = {fmaxf(x[n].x, 0.0f), fmaxf(x[n].y, 0.0f)};
+    x[n] = __builtin_elementwise_fma(-ax[n], r, m);
+  }
+}
+
 // clamp(round_half_even(v / s), -128, 127) with the reference's CORRECTLY ROUNDED quotient (fq_vit
 // quantizer/uniform.py:31-36), branch-free.  q0 = fl(v * inv) with inv = fl(1/s) can be ~1.5 ulp
 // off v/s -- outside Markstein's precondition (a faithful q) -- so one correction is not provably

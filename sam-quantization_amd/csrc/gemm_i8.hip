@@ -113,8 +113,11 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
   auto swz = [](int row) { return SWZ == 1 ? 4 * ((row >> 1) & 3) : SWZ == 2 ? 4 * ((row >> 1) & 1) : 0; };
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    // accumulator pairs (r, r + 1) = slice rows (rl, rl + 1): packed fp32; the whole slice's 8 x TN
+    // pairs are dequantised first and the GELU runs on all of them in lockstep (gelu_r16_n)
+    float2_t y[8 * TN];
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {   // accumulator pairs (r, r + 1) = slice rows (rl, rl + 1): packed fp32
+    for (int r = 0; r < 16; r += 2) {
       const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
       for (int t = 0; t < TN; ++t) {
@@ -123,8 +126,17 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
           a0 += __mul24(zpv[t], ssum[i * 32 + rl]);
           a1 += __mul24(zpv[t], ssum[i * 32 + rl + 1]);
         }
-        float2_t v = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]), (float2_t)(cb[t]));
-        if (GELU) v = gelu_r16_2(v);
+        y[(r / 2) * TN + t] = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]),
+                                                        (float2_t)(cb[t]));
+      }
+    }
+    if constexpr (GELU) gelu_r16_n<8 * TN>(y);
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const float2_t v = y[(r / 2) * TN + t];
         const int cs = (t * 32 + (lane & 31)) ^ swz(rl);   // rl even: swz(rl + 1) == swz(rl)
         ep[rl * WN + cs] = v.x;
         ep[(rl + 1) * WN + cs] = v.y;
