@@ -231,9 +231,8 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
 // the group is applied per byte in the unpack as for per-channel weights.  wscale is the f32
 // [G, N] scale table; the next group's zero / scale words are loaded one K tile ahead, before the
 // tile's LDS-DMA pieces (so the ring's counted vmcnt covers them).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS, bool GRP = false,
-          int WPE = 0>
-__global__ __launch_bounds__(64 * WAVES_M * WAVES_N) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1, 8)))
+template <int BM, int BN, int WAVES_M, int WAVES_N, int EPI, int BFMT, int STAGES, int AG = AG_ROWS, bool GRP = false>
+__global__ __launch_bounds__(64 * WAVES_M * WAVES_N)
 void i8_gemm_kernel(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
                     const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
                     const float* __restrict__ bias, void* __restrict__ Cout, int64_t ldc,
@@ -734,10 +733,10 @@ struct I8Args {
   const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep; I8Gather ga;
 };
 
-template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST, int AG = AG_ROWS, bool GRP = false, int WPE = 0>
+template <int BM, int BN, int WMW, int WNW, int EPI, int BF, int ST, int AG = AG_ROWS, bool GRP = false>
 static int launch_i8(const I8Args& a, hipStream_t st) {
   const int nwg = ((a.M + BM - 1) / BM) * (a.N / BN);
-  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST, AG, GRP, WPE>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
+  hipLaunchKernelGGL((i8_gemm_kernel<BM, BN, WMW, WNW, EPI, BF, ST, AG, GRP>), dim3(nwg), dim3(64 * WMW * WNW), 0, st,
                      a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias, a.C, a.ldc, a.M, a.N, a.K, a.ep, a.ga);
   SAMQ_LAUNCH_CHECK("i8_gemm launch");
   return SAMQ_OK;
@@ -793,18 +792,12 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 90: return launch_i8<64, 128, 2, 2, EPI, BF, 2>(a, st);
     case 91: return launch_i8<32, 64, 1, 2, EPI, BF, 2>(a, st);
     case 92: return launch_i8<64, 32, 2, 1, EPI, BF, 2>(a, st);
-#ifdef SAMQ_TUNING
-    case 120: return launch_i8<128, 256, 1, 4, EPI, BF, 2, AG_ROWS, false, 2>(a, st);
-    case 121: return launch_i8<256, 128, 2, 2, EPI, BF, 2, AG_ROWS, false, 2>(a, st);
-    case 122: return launch_i8<128, 256, 2, 4, EPI, BF, 2>(a, st);
-#endif
     default: return fail(SAMQ_ERR_INVALID, "i8_gemm: unknown tile config");
   }
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: case 120: case 122: return 256;
-    case 83: case 88: case 90: case 121: return 128; case 84: case 87: case 89: case 91: return 64;
+  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
     case 92: return 32; default: return 0; }
 }
 

@@ -19,7 +19,11 @@
 #   ab48=<variants>        in-graph W4A8 per-layer cfg A/B (tools/bench_cfg_ab_w4a8.py, tuning library)
 #   ab16=<variants>        in-graph W4A16 per-layer cfg A/B (tools/bench_cfg_ab.py, tuning library)
 #   abl=<mode>@<lib.so>    bench <mode> alternating this build and <lib.so> (SAMQ_LIB), 2 rounds each
+#   lanes=<mode>@<l1,l2..> bench <mode> at each lane count (2 rounds each, alternating)
 #   attn                   attention kernels isolated (tools/bench_attn.py)
+#   attnq8                 W8A8 attention kernels isolated (tools/bench_attn_q8.py)
+#   attnq8pmc              W8A8 attention counters (tools/attn_q8_pmc.sh)
+#   attnq8prof             W8A8 attention kernel trace (per-kernel durations, rocprofv3 --stats)
 #   probe                  v_cvt_pk_u8_f32 semantics (tools/probe_cvt_u8.hip, built on the box)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -80,7 +84,22 @@ for step in "$@"; do
               for f in gpurun_out/$tag.abl_${m}_*.log; do
                 echo "$f $(grep -h '"value"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
               done ;;
+    lanes=*)  m=${arg%@*}; ls=${arg#*@}
+              for r in 1 2; do
+                for l in ${ls//,/ }; do
+                  run lanes_${m}_${l}_$r 400 python bench.py --mode "$m" --lanes "$l" --steps 10 --warmup 3 --no-cpu-baseline --no-isolated
+                done
+              done
+              for f in gpurun_out/$tag.lanes_${m}_*.log; do
+                echo "$f $(grep -h '"value"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+              done ;;
     attn)     run attn 300 python -u tools/bench_attn.py ;;
+    attnq8)   run attnq8 300 python -u tools/bench_attn_q8.py ;;
+    attnq8pmc) run attnq8pmc 300 bash tools/attn_q8_pmc.sh ;;
+    attnq8prof) run attnq8prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$tag.attnq8prof -o run --output-format csv \
+                -- python3 tools/bench_attn_q8.py
+              python3 -c "import csv,sys; [print(r['Name'][:90], r['Calls'], r['AverageNs']) for r in csv.DictReader(open(sys.argv[1]))]" \
+                gpurun_out/$tag.attnq8prof/run_kernel_stats.csv ;;
     probe)    run probe 120 bash -c "hipcc --offload-arch=gfx950 -O2 -o gpurun_out/probe_cvt_u8 tools/probe_cvt_u8.hip && gpurun_out/probe_cvt_u8" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
