@@ -82,12 +82,14 @@ __global__ void w8_repack_kernel(const int8_t* __restrict__ w, int8_t* __restric
 // the full-rate 24-bit multiply: |zp| <= 16, |S| <= 128 K < 2^23)
 // Grouped W4 (float accumulators, the group scales already applied): wscale == nullptr, the
 // factor is a_scale alone.
+// One 32-row slice i of the wave's accumulator tile (i8_epilogue runs all TM of them; the
+// tile ping-pong kernel spreads them over the other group's main loop).
 template <int TM, int TN, int WN, int EPI, bool ZPS = false, typename AccV = int16_t_v>
-__device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int (&col)[TN],
-                                            const float* __restrict__ wscale, const float* __restrict__ bias,
-                                            const I8Epi& ep_args, float* ep, void* __restrict__ Cout, int64_t ldc,
-                                            int M, int row_base, int col_base, int lane,
-                                            const int* ssum = nullptr, const int* zpv = nullptr) {
+__device__ __forceinline__ void i8_epilogue_slice(int i, const AccV (&acc)[TM][TN], const int (&col)[TN],
+                                                  const float* __restrict__ wscale, const float* __restrict__ bias,
+                                                  const I8Epi& ep_args, float* ep, void* __restrict__ Cout,
+                                                  int64_t ldc, int M, int row_base, int col_base, int lane,
+                                                  const int* ssum = nullptr, const int* zpv = nullptr) {
   const int hsel = lane >> 5;
   float csc[TN], cb[TN];
 #pragma unroll
@@ -111,35 +113,37 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
   constexpr bool F16OUT = EPI == SAMQ_EPI_BIAS || EPI == SAMQ_EPI_BIAS_GELU;
   constexpr int SWZ = (Q8OUT && WN % 16 == 0) ? 1 : (F16OUT && WN % 8 == 0) ? 2 : 0;
   auto swz = [](int row) { return SWZ == 1 ? 4 * ((row >> 1) & 3) : SWZ == 2 ? 4 * ((row >> 1) & 1) : 0; };
+  {
+    // accumulator pairs (r, r + 1) = slice rows (rl, rl + 1): packed fp32; four rows x TN columns
+    // at a time are dequantised and their GELU chains run in lockstep (gelu_r16_n: 2 TN pairs)
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    // accumulator pairs (r, r + 1) = slice rows (rl, rl + 1): packed fp32; the whole slice's 8 x TN
-    // pairs are dequantised first and the GELU runs on all of them in lockstep (gelu_r16_n)
-    float2_t y[8 * TN];
+    for (int r0 = 0; r0 < 16; r0 += 4) {
+      float2_t y[2 * TN];
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+      for (int r = r0; r < r0 + 4; r += 2) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        auto a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
-        if constexpr (ZPS) {   // v_mad_i32_i24 (zpv = -zp; |S| <= 128 K < 2^23: K < 65536 checked at launch)
-          a0 += __mul24(zpv[t], ssum[i * 32 + rl]);
-          a1 += __mul24(zpv[t], ssum[i * 32 + rl + 1]);
+        for (int t = 0; t < TN; ++t) {
+          auto a0 = acc[i][t][r], a1 = acc[i][t][r + 1];
+          if constexpr (ZPS) {   // v_mad_i32_i24 (zpv = -zp; |S| <= 128 K < 2^23: K < 65536 checked at launch)
+            a0 += __mul24(zpv[t], ssum[i * 32 + rl]);
+            a1 += __mul24(zpv[t], ssum[i * 32 + rl + 1]);
+          }
+          y[((r - r0) / 2) * TN + t] = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]),
+                                                                 (float2_t)(cb[t]));
         }
-        y[(r / 2) * TN + t] = __builtin_elementwise_fma((float2_t){(float)a0, (float)a1}, (float2_t)(csc[t]),
-                                                        (float2_t)(cb[t]));
       }
-    }
-    if constexpr (GELU) gelu_r16_n<8 * TN>(y);
+      if constexpr (GELU) gelu_r16_n<2 * TN>(y);
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+      for (int r = r0; r < r0 + 4; r += 2) {
+        const int rl = (r & 3) + 8 * (r >> 2) + 4 * hsel;
 #pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        const float2_t v = y[(r / 2) * TN + t];
-        const int cs = (t * 32 + (lane & 31)) ^ swz(rl);   // rl even: swz(rl + 1) == swz(rl)
-        ep[rl * WN + cs] = v.x;
-        ep[(rl + 1) * WN + cs] = v.y;
+        for (int t = 0; t < TN; ++t) {
+          const float2_t v = y[((r - r0) / 2) * TN + t];
+          const int cs = (t * 32 + (lane & 31)) ^ swz(rl);   // rl even: swz(rl + 1) == swz(rl)
+          ep[rl * WN + cs] = v.x;
+          ep[(rl + 1) * WN + cs] = v.y;
+        }
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -221,6 +225,18 @@ __device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
+}
+
+template <int TM, int TN, int WN, int EPI, bool ZPS = false, typename AccV = int16_t_v>
+__device__ __forceinline__ void i8_epilogue(const AccV (&acc)[TM][TN], const int (&col)[TN],
+                                            const float* __restrict__ wscale, const float* __restrict__ bias,
+                                            const I8Epi& ep_args, float* ep, void* __restrict__ Cout, int64_t ldc,
+                                            int M, int row_base, int col_base, int lane,
+                                            const int* ssum = nullptr, const int* zpv = nullptr) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+    i8_epilogue_slice<TM, TN, WN, EPI, ZPS, AccV>(i, acc, col, wscale, bias, ep_args, ep, Cout, ldc, M, row_base,
+                                                  col_base, lane, ssum, zpv);
 }
 
 // ------------------------------------------------------------------ GEMM
@@ -728,6 +744,248 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
                                m0 + wm * WM, n0 + wn * WN, lane);
 }
 
+// ------------------------------------------------------------------ W4A8 tile ping-pong GEMM (round 5)
+// TUNING BUILD ONLY (cfg 99): bit-identical to cfg 86 on every epilogue (tests/test_w8a8.py with the
+// tuning library), but 1.67x slower at M = 16384 (781 vs 467 us per ViT-H block,
+// profiles/r5_i8_decomposition.log): one MFMA wave per SIMD that also reads its own fragments and
+// issues ten LDS-DMA pieces per K step runs that step at ~20 % of the MFMA rate, and the epilogue it
+// hides is smaller than what it loses.  Kept as the measured form of the verdict's option (b).
+#ifdef SAMQ_TUNING
+// The epilogue of one tile under the main loop of the next.  i8_gemm_pp2 alternates its two wave
+// groups PHASE by phase inside one 256x256 tile, so both groups reach the epilogue together and
+// the MFMA pipes idle through it (a third of the W4A8 GEMM time, profiles/r5_i8_decomposition.log:
+// epilogues 158 of 472 us per ViT-H block at M = 16384).  Here the groups alternate TILE by tile:
+// a workgroup owns P consecutive 256x128 tiles; group (j & 1) runs the main loop of its tile j (4
+// waves, one per SIMD, 128x64 each) while the other group -- its SIMD partners -- (a) runs the
+// epilogue of ITS tile j - 1 in four 32-row slices spread over tile j's K steps and (b) sums the
+// int8 rows of tile j's staged A (the zero point through row sums, as cfg 86: acc = sum a * q,
+// epilogue subtracts zp[n] * S[m]; integer-exact, bit-identical to cfg 86) -- so the MFMA issue of
+// one wave and the VALU / store work of the other share each SIMD.  One K-step stream over the P
+// tiles feeds a 3-slot LDS-DMA ring (40 KiB stages: 32 KiB A + 8 KiB layout-3 B), lookahead 2,
+// issued by the main-loop group (ten 1-KiB pieces per wave per step, spread through its MFMAs);
+// one barrier per K step.  vmcnt: a wave that issued pieces in the previous step and no stores
+// since waits vmcnt(10) (the newest step's pieces may stay in flight), otherwise vmcnt(0).
+template <int EPI>
+__global__ __launch_bounds__(512, 1)
+void i8_gemm_tpp(const int8_t* __restrict__ A, int64_t lda, const char* __restrict__ Wp,
+                 const float* __restrict__ wscale, const uint32_t* __restrict__ qzeros,
+                 const float* __restrict__ bias, void* __restrict__ Cout, int64_t ldc, int M, int N, int K,
+                 I8Epi ep_args, int P) {
+  constexpr int TM = 4, TN = 2, WM = 128, WN = 64, BM = 256, BN = 128, BK = 128, ROWB = BK;
+  constexpr int A_BYTES = BM * ROWB, NA = BM / 8, NB = (BN / 32) * 2, NT = NA + NB, NPW = NT / 4;
+  constexpr int STAGE = A_BYTES + NB * 1024, STAGES = 3, LA = 2;
+  constexpr int EP_BYTES = 32 * WN * 4;
+  constexpr int EP_OFF = STAGES * STAGE, RS_OFF = EP_OFF + 4 * EP_BYTES;
+  constexpr int SMEM = RS_OFF + 2 * BM * 4;
+  static_assert(NT % 4 == 0 && SMEM <= 160 * 1024, "tile ping-pong layout");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  int* rsl = (int*)(smem + RS_OFF);   // [2][BM] row sums of the tiles, by tile parity
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, gw = wave & 3, wm = gw >> 1, wn = gw & 1;
+  const int hsel = lane >> 5;
+  const int tiles_n = N / BN, tiles_m = (M + BM - 1) / BM, tiles = tiles_m * tiles_n;
+  const int nwg = (tiles + P - 1) / P;
+  const int t0 = xcd_remap(blockIdx.x, nwg) * P;
+  const int nt = tiles - t0 < P ? tiles - t0 : P;   // tiles of this workgroup (>= 1)
+  const int KT = K / BK, S = nt * KT;
+  auto tile_mn = [&](int j, int& m0, int& n0) {
+    const int u = t0 + j;
+    m0 = (u / tiles_n) * BM;
+    n0 = (u % tiles_n) * BN;
+  };
+  // DMA pieces of stream step q (ML group waves only): this wave's NPW 32-bit source offsets
+  // (A rows or packed B blocks, both < 2^31 bytes: checked at launch) computed once per step,
+  // then issued a few at a time between the MFMAs
+  auto piece_offsets = [&](int q, uint32_t (&off)[NPW]) {
+    const int j = q / KT, kt = q - j * KT;
+    int m0, n0;
+    tile_mn(j, m0, n0);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int pc = gw * NPW + i;   // uniform: A pieces for gw < 3, B for gw == 3 (NA = 32 = 3 * 10 + 2)
+      if (pc < NA) {
+        const int row = pc * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        int gr = m0 + row;
+        gr = gr < M ? gr : M - 1;
+        off[i] = (uint32_t)((int64_t)gr * lda + kt * BK + c * 16);
+      } else {
+        const int jb = pc - NA, nb = n0 / 32 + jb / 2;
+        off[i] = (uint32_t)((((int64_t)nb * KT + kt) * 2 + (jb & 1)) * 1024 + lane * 16);
+      }
+    }
+  };
+  auto issue = [&](int q, const uint32_t (&off)[NPW], int i0, int i1) {
+    char* sl = smem + (q % STAGES) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      if (i < i0 || i >= i1) continue;
+      const int pc = gw * NPW + i;
+      const char* src = pc < NA ? (const char*)A + off[i] : Wp + off[i];
+      const int dst = pc < NA ? pc * 1024 : A_BYTES + (pc - NA) * 1024;
+      __builtin_amdgcn_global_load_lds((const SAMQ_GLOBAL void*)src, (SAMQ_LDS void*)(sl + dst), 16, 0, 0);
+    }
+  };
+
+  int16_t_v acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][t][r] = 0;
+  int a_off[TM], a_swz[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rr = wm * WM + i * 32 + (lane & 31);
+    a_off[i] = rr * ROWB;
+    a_swz[i] = (rr >> 1) & 7;
+  }
+  uint32_t kLo = 0x0F0F0F0Fu;
+  asm volatile("" : "+v"(kLo));
+  const int rs_row = gw * 64 + lane;                 // EPI role: the row of the ML tile this lane sums
+  int rsum = 0;
+
+  // prologue: group 0 runs tile 0's main loop; it stages steps 0 .. LA - 1
+  if (grp == 0) {
+    uint32_t off[NPW];
+    piece_offsets(0, off);
+    issue(0, off, 0, NPW);
+    if (S > 1) {
+      piece_offsets(1, off);
+      issue(1, off, 0, NPW);
+    }
+  }
+  int issued_prev = grp == 0 ? (S > 1 ? NPW : 0) : 0;   // pieces this wave issued in the previous step
+  bool stores = false;                                  // global stores since this wave's last vmcnt(0)
+  int epi_j = -1;                                       // the tile whose epilogue this wave owes
+
+  for (int q = 0; q < S; ++q) {
+    const int j = q / KT, kt = q - j * KT;
+    const bool ml = (j & 1) == grp;
+    // ---- step q's pieces landed (this wave's), then every wave's
+    if (issued_prev > 0 && !stores) {
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      stores = false;
+    }
+    __builtin_amdgcn_s_barrier();   // step q staged; the last step's row sums / LDS reads done
+    const char* st = smem + (q % STAGES) * STAGE;
+    if (ml) {
+      // ---------------- main loop step: 4 k32 steps x 8 MFMAs, the next-next step's pieces spread
+      if (kt == 0) {   // a new tile: the accumulators start from zero (their last epilogue slice is done)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][t][r] = 0;
+      }
+      const bool pf = q + LA < S;
+      uint32_t poff[NPW];
+      if (pf) piece_offsets(q + LA, poff);
+      u32x4 bw[TN][2];
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) bw[t][pp] = *(const u32x4*)(st + A_BYTES + ((wn * TN + t) * 2 + pp) * 1024 + lane * 16);
+      static_for<4>([&](auto sc_) {
+        constexpr int sk = decltype(sc_)::value;
+        int4_t af[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *(const int4_t*)(st + a_off[i] + (((2 * sk + hsel) ^ a_swz[i]) << 4));
+        int4_t bf[TN];
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          const uint32_t w0 = bw[t][sk >> 1][2 * (sk & 1)], w1 = bw[t][sk >> 1][2 * (sk & 1) + 1];
+          bf[t] = int4_t{(int)(w0 & kLo), (int)((w0 >> 4) & kLo), (int)(w1 & kLo), (int)((w1 >> 4) & kLo)};
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int t = 0; t < TN; ++t) {
+            acc[i][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[t], acc[i][t], 0, 0, 0);
+          }
+        // pieces of step q + LA: 2-3 behind each k32 step's MFMAs
+        constexpr int I0 = (sk * NPW) / 4, I1 = ((sk + 1) * NPW) / 4;
+        __builtin_amdgcn_sched_barrier(0);
+        if (pf) issue(q + LA, poff, I0, I1);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      issued_prev = pf ? NPW : 0;
+      if (kt == KT - 1) epi_j = j;   // this tile's epilogue runs under the next tile's main loop
+    } else {
+      issued_prev = 0;
+      // ---------------- row sums of the ML tile's staged A (rows 64 gw .. +63, one per lane)
+      {
+        const char* rp = st + rs_row * ROWB;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int4_t x = *(const int4_t*)(rp + (((c + (rs_row >> 1)) & 7) << 4));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rsum = __builtin_amdgcn_sdot4(x[e], 0x01010101, rsum, false);
+        }
+        if (kt == KT - 1) {
+          rsl[(j & 1) * BM + rs_row] = rsum;
+          rsum = 0;
+        }
+      }
+      // ---------------- epilogue slices of this wave's previous tile (needs its row sums: written
+      // at that tile's last step by the other group, visible after this step's barrier)
+      int sl = -1;   // the slice of the owed epilogue due at this step (slices at K steps i KT / 4)
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+        if (kt == (ii * KT) / TM) sl = ii;
+      if (epi_j >= 0 && sl >= 0) {
+        int m0, n0;
+        tile_mn(epi_j, m0, n0);
+        int col[TN], zpv[TN];
+#pragma unroll
+        for (int t = 0; t < TN; ++t) {
+          col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+          const uint32_t zw = qzeros[col[t] >> 3];
+          zpv[t] = -(int)(((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u);
+        }
+        // the due slice by a uniform switch: constant register indices, the accumulators only read
+        float* epw = (float*)(smem + EP_OFF + gw * EP_BYTES);
+        const int* rsp = rsl + (epi_j & 1) * BM + wm * WM;
+        switch (sl) {
+          case 0: i8_epilogue_slice<TM, TN, WN, EPI, true>(0, acc, col, wscale, bias, ep_args, epw, Cout, ldc, M,
+                                                           m0 + wm * WM, n0 + wn * WN, lane, rsp, zpv); break;
+          case 1: i8_epilogue_slice<TM, TN, WN, EPI, true>(1, acc, col, wscale, bias, ep_args, epw, Cout, ldc, M,
+                                                           m0 + wm * WM, n0 + wn * WN, lane, rsp, zpv); break;
+          case 2: i8_epilogue_slice<TM, TN, WN, EPI, true>(2, acc, col, wscale, bias, ep_args, epw, Cout, ldc, M,
+                                                           m0 + wm * WM, n0 + wn * WN, lane, rsp, zpv); break;
+          default: i8_epilogue_slice<TM, TN, WN, EPI, true>(3, acc, col, wscale, bias, ep_args, epw, Cout, ldc, M,
+                                                            m0 + wm * WM, n0 + wn * WN, lane, rsp, zpv); break;
+        }
+        stores = true;
+        if (sl == TM - 1) epi_j = -1;   // done; the accumulators restart at the next main-loop tile
+      }
+    }
+  }
+  // ---- tail: the last tile's epilogue (its group ran its main loop last; the row sums were written
+  // at the last step by the other group)
+  __syncthreads();
+  if (epi_j >= 0) {
+    int m0, n0;
+    tile_mn(epi_j, m0, n0);
+    int col[TN], zpv[TN];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) {
+      col[t] = n0 + wn * WN + t * 32 + (lane & 31);
+      const uint32_t zw = qzeros[col[t] >> 3];
+      zpv[t] = -(int)(((zw >> (4 * (col[t] & 7))) & 0xFu) + 1u);
+    }
+    i8_epilogue<TM, TN, WN, EPI, true>(acc, col, wscale, bias, ep_args, (float*)(smem + EP_OFF + gw * EP_BYTES), Cout,
+                                       ldc, M, m0 + wm * WM, n0 + wn * WN, lane, rsl + (epi_j & 1) * BM + wm * WM, zpv);
+  }
+}
+#endif  // SAMQ_TUNING
+
 struct I8Args {
   const int8_t* A; int64_t lda; const char* Wp; const float* wscale; const uint32_t* qzeros;
   const float* bias; void* C; int64_t ldc; int M, N, K; I8Epi ep; I8Gather ga;
@@ -741,6 +999,23 @@ static int launch_i8(const I8Args& a, hipStream_t st) {
   SAMQ_LAUNCH_CHECK("i8_gemm launch");
   return SAMQ_OK;
 }
+
+#ifdef SAMQ_TUNING
+template <int EPI>
+static int launch_i8_tpp(const I8Args& a, hipStream_t st) {
+  SAMQ_REQUIRE(a.K < 65536 && a.K / 128 >= 4, SAMQ_ERR_UNSUPPORTED,
+               "w4a8_gemm: the tile ping-pong needs 512 <= K < 65536 (four epilogue slices per tile's K steps)");
+  SAMQ_REQUIRE((int64_t)a.M * a.lda < (int64_t)1 << 31 && (int64_t)a.K * a.N / 2 < (int64_t)1 << 31, SAMQ_ERR_UNSUPPORTED,
+               "w4a8_gemm: the tile ping-pong addresses A and the weights with 31-bit offsets");
+  const int tiles = ((a.M + 255) / 256) * (a.N / 128);
+  const int P = tiles >= 4 * 256 ? 4 : 2;   // tiles per workgroup (even: both groups run main loops)
+  const int nwg = (tiles + P - 1) / P;
+  hipLaunchKernelGGL((i8_gemm_tpp<EPI>), dim3(nwg), dim3(512), 0, st, a.A, a.lda, a.Wp, a.wscale, a.qzeros, a.bias,
+                     a.C, a.ldc, a.M, a.N, a.K, a.ep, P);
+  SAMQ_LAUNCH_CHECK("i8_gemm_tpp launch");
+  return SAMQ_OK;
+}
+#endif
 
 template <int EPI, int STAGES, int LA, int VAR = 0>
 static int launch_i8_pp2(const I8Args& a, hipStream_t st) {
@@ -769,6 +1044,9 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 93 is the W4 ping-pong kernel");
 #ifdef SAMQ_TUNING
+    case 99:   // tile ping-pong: one group's epilogue under the other group's main loop (correct, slower)
+      if constexpr (BF == BF_W4) return launch_i8_tpp<EPI>(a, st);
+      else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 99 is a W4 kernel");
     case 94:   // timing-only: cfg 86 without its epilogue
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 32>(a, st);
       return fail(SAMQ_ERR_INVALID, "i8_gemm: W4 only");
@@ -797,7 +1075,7 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: return 128; case 84: case 87: case 89: case 91: return 64;
+  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: case 99: return 128; case 84: case 87: case 89: case 91: return 64;
     case 92: return 32; default: return 0; }
 }
 
