@@ -573,10 +573,15 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
 // row: the height term is one value per block and the width term a fixed per-lane set (kw = 4 g + i,
 // registers) -- per score no index decode and no table reads, unlike the generic path above.
 // Scores, quantisers, softmax and P.V (hi + lo fp16, tr-read V, MFMA row sums) as the row64 kernel.
-template <int SW>
-// two workgroups per CU: LDS <= 80 KiB and (HIP's second bound = waves per SIMD) <= 512 / 7 VGPRs
-__global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_win_kernel(AttnQ8Params p) {
-  constexpr int NWQ = SW, SLOTS = 16 * SW, VP = QD + 8;
+// NWQ < SW (round 5): a workgroup takes NWQ of the window's SW query rows (blockIdx.z = which NWQ),
+// each staging the whole window's K / V: 14 x 14 windows of vit_b at B = 1 are 300 (window, head)
+// items on 256 CUs, so 44 CUs ran two whole items one after the other; as 600 half-items of 7 waves
+// the load spreads as ~2.3 half-items per CU.
+template <int SW, int NWQ = SW>
+// two workgroups per CU: LDS <= 80 KiB and (HIP's second bound = waves per SIMD) <= 512 / (waves / 2) VGPRs
+__global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_win_kernel(AttnQ8Params p) {
+  constexpr int SLOTS = 16 * SW, VP = QD + 8;
+  static_assert(SW % NWQ == 0, "query rows split evenly");
   constexpr int NCH = (SW + 3) / 4;                        // chunks of up to 4 key rows (64 slots)
   static_assert(SW <= 16, "one window per workgroup");
   __shared__ __attribute__((aligned(16))) int8_t k_lds[SLOTS * KPITCH];
@@ -636,7 +641,7 @@ __global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_wi
   // ---- this wave's query row qy = wave (queries qx = ql < S) and its rel-pos terms (MFMA, rows
   // qy - k + S - 1 for both tables: quirk 1); rel_w for kw = 4 g + i into registers
   const bool q_in = ql < SW;
-  const int qy = wave, qx = q_in ? ql : 0;
+  const int qy = blockIdx.z * NWQ + wave, qx = q_in ? ql : 0;
   bool q_ok = false;
   int4v qfrag = {0, 0, 0, 0};
   if (q_in) {
@@ -668,7 +673,7 @@ __global__ __launch_bounds__(64 * SW, (2 * SW + 3) / 4) void rel_attention_q8_wi
   static_assert(sizeof(q_lds) >= PTAB * 4, "P table alias");
   uint32_t* ptab = (uint32_t*)&q_lds[0][0];
   const int lazyc = q8_ptab_lazy(p.k2);
-  q8_ptab_fill<64 * SW>(ptab, p.k2, lazyc, tid);
+  q8_ptab_fill<64 * NWQ>(ptab, p.k2, lazyc, tid);
   __syncthreads();
   const float* rhq = &rh_lds[wave][ql * (SW + 1)];
 
@@ -798,8 +803,10 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.nwh = (H + window - 1) / window; p.nww = (W + window - 1) / window;
     p.L = window * window;
     const dim3 grid(B * p.nwh * p.nww, heads, 1);
-    if (window == 14)     // SAM's 14 x 14 windows: key and query rows of 16 slots
-      hipLaunchKernelGGL((rel_attention_q8_win_kernel<14>), grid, dim3(64 * 14), 0, stream, p);
+    if (window == 14) {   // SAM's 14 x 14 windows: key and query rows of 16 slots, half a window per workgroup
+      const dim3 grid2(B * p.nwh * p.nww, heads, 2);
+      hipLaunchKernelGGL((rel_attention_q8_win_kernel<14, 7>), grid2, dim3(64 * 7), 0, stream, p);
+    }
     else if (p.L <= 13 * 16)
       hipLaunchKernelGGL((rel_attention_q8_kernel<true, 13, 256, 16>), grid, dim3(64 * 13), 0, stream, p);
     else
