@@ -56,17 +56,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# committed PMC passes (tools/pmc_all.sh) per (mode, GEMM rows per launch)
-PMC_PROFILES = {("w4a16", 16384): "r1_pmc_traffic_w4a16.json", ("w4a16", 8192): "r4_pmc_traffic_w4a16_m8192.json",
-                ("w4a8", 16384): "r4_pmc_traffic_w4a8_m16384.json", ("w8a8", 4096): "r4_pmc_traffic_w8a8_m4096.json"}
+# committed PMC passes (tools/pmc_all.sh) per (mode, GEMM rows per launch), newest round first
+PMC_PROFILES = {("w4a16", 16384): ["r1_pmc_traffic_w4a16.json"],
+                ("w4a16", 8192): ["r5_pmc_traffic_w4a16_m8192.json", "r4_pmc_traffic_w4a16_m8192.json"],
+                ("w4a8", 16384): ["r5_pmc_traffic_w4a8_m16384.json", "r4_pmc_traffic_w4a8_m16384.json"],
+                ("w8a8", 4096): ["r5_pmc_traffic_w8a8_m4096.json", "r4_pmc_traffic_w8a8_m4096.json"]}
 
 
-def pmc_traffic(mode: str, profile: str):
+def pmc_traffic(mode: str, profiles):
     """HBM bytes per launch of the mode's projection GEMMs (``is_proj_gemm``; dispatch-weighted
-    average) from a committed rocprofv3 PMC summary (tools/pmc_all.sh -> profiles/*.json), or None."""
-    f = REPO / "profiles" / profile
-    if not f.exists():
+    average) from the newest committed rocprofv3 PMC summary (tools/pmc_all.sh -> profiles/*.json),
+    or None."""
+    found = [p for p in ([profiles] if isinstance(profiles, str) else profiles) if (REPO / "profiles" / p).exists()]
+    if not found:
         return None, None
+    profile = found[0]
+    f = REPO / "profiles" / profile
     d = json.loads(f.read_text())
     tot = n = 0
     for k, v in d["kernels"].items():

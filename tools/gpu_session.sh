@@ -12,6 +12,9 @@
 #   benchq | b48q | b88q   bench lines without CPU baseline
 #   instep | instep48 | instep88 | instepg   rocprofv3 in-step kernel traces (tools/instep_profile.sh)
 #   pmc                    PMC HBM traffic of every mode (tools/pmc_all.sh)
+#   publish=<round>        copy this build's in-step traces and the PMC summaries (wrapped with their
+#                          source line as profiles/<round>_pmc_traffic_<mode>_m<rows>.json) into
+#                          profiles/, so later bench steps in the same call quote them
 #   attnpmc                attention counters (tools/attn_pmc.sh)
 #   pmci8                  int8 GEMM counters (tools/pmc_i8.sh)
 #   i8=<cfgs>@<m>          int8 GEMM tile configs (tools/bench_i8.py, tuning library)
@@ -68,6 +71,22 @@ for step in "$@"; do
     instep88) run instep88 500 bash tools/instep_profile.sh w8a8 ;;
     instepg)  run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128 ;;
     pmc)      run pmc 900 bash tools/pmc_all.sh ;;
+    publish=*) H=$(python3 -c "import bench; print(bench.source_hash())")
+              cp gpurun_out/instep_*_"$H".json gpurun_out/instep_*_"$H"_wholerun_stats.csv profiles/ || exit 1
+              for mr in w4a16:8192 w4a8:16384 w8a8:4096; do
+                python3 - "${mr%:*}" "${mr#*:}" "$H" "$arg" <<'PY' || exit 1
+import json, sys
+m, r, h, rnd = sys.argv[1:]
+src = (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, tools/pmc_all.sh via tools/gpu_session.sh) "
+       f"over `python3 bench.py --mode {m} --steps 2 --warmup 1 --no-cpu-baseline --no-graph` (GEMM M = {r} per "
+       f"launch) on MI355X, build {h}; hbm = 2*FETCH_SIZE + WRITE_SIZE per dispatch (MI355X_MICROARCH.md HBM "
+       f"section: gfx950 FETCH_SIZE counts half of 16-B/lane streaming reads; Infinity-Cache hits included)")
+out = {"source": src, "kernels": json.load(open(f"gpurun_out/pmc_{m}.json"))}
+for d in ("gpurun_out", "profiles"):
+    json.dump(out, open(f"{d}/{rnd}_pmc_traffic_{m}_m{r}.json", "w"), indent=1)
+PY
+              done
+              ls -l profiles/instep_*_"$H"* profiles/"$arg"_pmc_traffic_* ;;
     attnpmc)  run attnpmc 400 bash tools/attn_pmc.sh ;;
     pmci8)    run pmci8 400 bash tools/pmc_i8.sh ;;
     i8=*)     run i8_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_i8.py \
