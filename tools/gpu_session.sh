@@ -14,7 +14,8 @@
 #   pmc                    PMC HBM traffic of every mode (tools/pmc_all.sh)
 #   publish=<round>        copy this build's in-step traces and the PMC summaries (wrapped with their
 #                          source line as profiles/<round>_pmc_traffic_<mode>_m<rows>.json) into
-#                          profiles/, so later bench steps in the same call quote them
+#                          profiles/, so later bench steps in the same call quote them; copies of
+#                          them come back in gpurun_out/publish_<round>/ (raw trace dirs removed)
 #   attnpmc                attention counters (tools/attn_pmc.sh)
 #   pmci8                  int8 GEMM counters (tools/pmc_i8.sh)
 #   i8=<cfgs>@<m>          int8 GEMM tile configs (tools/bench_i8.py, tuning library)
@@ -86,7 +87,11 @@ for d in ("gpurun_out", "profiles"):
     json.dump(out, open(f"{d}/{rnd}_pmc_traffic_{m}_m{r}.json", "w"), indent=1)
 PY
               done
-              ls -l profiles/instep_*_"$H"* profiles/"$arg"_pmc_traffic_* ;;
+              # the raw rocprofv3 directories would push gpurun_out/ past what comes back from the box
+              find gpurun_out -mindepth 1 -maxdepth 1 -type d \( -name 'instep_*' -o -name 'pmc_*' \) -exec rm -rf {} +
+              mkdir -p gpurun_out/publish_"$arg"
+              cp profiles/instep_*_"$H"* profiles/"$arg"_pmc_traffic_* gpurun_out/publish_"$arg"/
+              ls -l gpurun_out/publish_"$arg" ;;
     attnpmc)  run attnpmc 400 bash tools/attn_pmc.sh ;;
     pmci8)    run pmci8 400 bash tools/pmc_i8.sh ;;
     i8=*)     run i8_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_i8.py \
