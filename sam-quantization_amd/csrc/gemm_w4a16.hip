@@ -1266,8 +1266,8 @@ __device__ __forceinline__ void xcd_tile(int bid, int tiles_m, int tiles_n, bool
 template <int WAVES_M, int TM, int TN, int STAGES, int EPI, int VAR>
 struct Pp2Lds {
   static constexpr int NW = 8, WM = TM * 32, WN = TN * 32, BM = WAVES_M * WM, BN = (NW / WAVES_M) * WN;
-  static constexpr bool GR = (VAR & 512) != 0, M16 = (VAR & 16) != 0;
-  static constexpr int GRB = GR ? (BN * 2 / 16 + BN / 32) * 16 : 0;
+  static constexpr bool GR = (VAR & 512) != 0, M16 = (VAR & 16) != 0, GRR = GR && (VAR & (1 << 23)) != 0;
+  static constexpr int GRB = GR && !GRR ? (BN * 2 / 16 + BN / 32) * 16 : 0;
   static constexpr int STAGE = BM * 128 + (BN / 32) * 1024 + GRB;
   static constexpr int EP_BYTES = M16 ? 16 * (WN + 4) * 4 : (WN > 64 ? 16 : 32) * WN * 4;
   static constexpr int RI_BYTES = (EPI == SAMQ_EPI_BIAS_LNF || EPI == SAMQ_EPI_GELU_LNF) ? BM * 8 : 0;
@@ -1309,12 +1309,22 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   // phase 0.  The unpack scales the exact integers once in fp16, fp16((q - zp) * s) (the v3
   // kernels' semantics); the epilogue's per-channel scale is 1.
   constexpr bool GR = (VAR & 512) != 0;
+  // VAR & (1 << 23) (with GR), register rows: each lane loads its own columns' group scale and zero
+  // word straight into VGPRs (global loads in inline asm, so the compiler adds no wait of its own --
+  // its waitcnt pass would wait vmcnt(0) on the loop-carried registers, round 3), issued in the
+  // MFMA half of a group's first K tile for the NEXT group, before that phase's LDS-DMA pieces.
+  // They count in the ring's vmcnt arithmetic (gl below) and a counted wait at the next group's
+  // start retires them.  The ring then carries no group row: 4 slots / lookahead 3 like the
+  // per-channel cfg 57, instead of 3 / 2 (4 x 40 KiB fill the 160 KiB LDS).
+  constexpr bool GRR = GR && (VAR & (1 << 23)) != 0;
   // timing-only (tuning build): VAR & 1024 skips the fp16 group scaling, VAR & 2048 the group row
   constexpr bool G_NOSCALE = (VAR & 1024) != 0, G_NOROW = (VAR & 2048) != 0;
   constexpr int GLS = BN * 2 / 16, GLZ = BN / 32;   // lanes carrying scales / zero words
   static_assert(!GR || GLS + GLZ <= 64, "group row: one lane per 16 bytes");
-  constexpr int GRB = GR ? (GLS + GLZ) * 16 : 0;
-  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB + (GR ? 1 : 0);
+  constexpr bool GROW = GR && !GRR;                   // the group row rides in the ring
+  constexpr int GRB = GROW ? (GLS + GLZ) * 16 : 0;
+  constexpr int NA = BM / 8, NB = BN / 32, NT = NA + NB + (GROW ? 1 : 0);
+  constexpr int NGL = GRR ? 2 * TN * ((VAR & 16) ? 2 : 1) : 0;   // GRR: loads per lane per group
   constexpr int NPW = (NT + NW - 1) / NW;
   constexpr int STAGE = A_BYTES + NB * 1024 + GRB;
   constexpr int KPP = 4 / NPH;
@@ -1353,7 +1363,8 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   static_assert(!M16 || NPH <= 2, "M16: one or two phases per K tile");
   static_assert(NPH >= 1 && 4 % NPH == 0, "phases");
   static_assert(LA >= 2 && LA < STAGES, "ring");
-  static_assert((LA - 2) * NPW + PRE_LAST <= 63, "vmcnt");
+  static_assert((LA - 2) * (NPW + NGL) + PRE_LAST + NGL <= 63, "vmcnt");
+  static_assert(!GRR || 3 * NPW <= 63, "vmcnt (group start)");
   static_assert(SMEM <= 160 * 1024, "LDS");
 
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -1380,13 +1391,13 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   // VAR & 8192 (and GR): pieces dealt j = i * 8 + wave (interleaved) instead of wave * NPW + i;
   // GR: the A / B pieces fill slots i < NPW - 1; slot NPW - 1 of wave 0 is the group row
   constexpr bool ILV = GR || (VAR & 8192) != 0;
-  static_assert(!GR || ((NA + NB) % NW == 0 && NPW == (NA + NB) / NW + 1), "group row slot");
-  static_assert(!GR || pp2_pre(NPH - 1, NPW, NPH, 0) <= NPW - 1, "group row issued in the last phase");
+  static_assert(!GROW || ((NA + NB) % NW == 0 && NPW == (NA + NB) / NW + 1), "group row slot");
+  static_assert(!GROW || pp2_pre(NPH - 1, NPW, NPH, 0) <= NPW - 1, "group row issued in the last phase");
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     int j = ILV ? i * NW + wave : wave * NPW + i;
     j = j < NT ? j : NT - 1;
-    if (GR && i == NPW - 1) {
+    if (GROW && i == NPW - 1) {
       if (lane < GLS) {
         src[i] = (const char*)(scales + n0 + 8 * lane);
         step[i] = N * 2;
@@ -1415,7 +1426,7 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
 #pragma unroll
     for (int i = 0; i < NPW; ++i)
       if (i >= i0 && i < i1) {
-        if (GR && i == NPW - 1) {
+        if (GROW && i == NPW - 1) {
           // wave 0, and only for a K tile that starts a group (uniform: wave is an SGPR)
           if (!G_NOROW && wave == 0 && kt % kpg == 0) {
             if (lane < GLS + GLZ)
@@ -1431,7 +1442,7 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   // GR: the raw group row values of this lane's columns (read after the retire wait of their tile)
   // and the fp16 scale splats (set from them where a group starts)
   half2_t gsc[TN], gsc16[TN][2];
-  uint32_t graw_s[TN][2], graw_z[TN][2];
+  uint32_t graw_s[TN][2] = {}, graw_z[TN][2] = {};
   auto gread = [&](int slot_) {
     const char* gp = smem + slot_ * STAGE + A_BYTES + NB * 1024;
 #pragma unroll
@@ -1444,7 +1455,32 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
       }
   };
   // GR: LDS-DMA pieces this wave issues for K tile t (wave 0 adds the group row where a group starts)
-  auto npieces = [&](int t) -> int { return GR ? NPW - 1 + (wave == 0 && t % kpg == 0 ? 1 : 0) : NPW; };
+  auto npieces = [&](int t) -> int { return GROW ? NPW - 1 + (wave == 0 && t % kpg == 0 ? 1 : 0) : NPW; };
+  // GRR: the register-row loads of a group are issued in the MFMA half of the previous group's first
+  // tile t0, right before K tile t0 + LA's pieces; gl(kt + j) = such loads precede tile kt + j's
+  // pieces (t0 = kt + j - LA starts a group and a group follows it).  t0 % kpg from the position
+  // gk of tile kt in its group: (gk + j - LA) mod kpg, at most LA - 2 additions of kpg -- not a
+  // loop over t0 (that SALU chain sat in every last-phase load half: lin2, 80 K tiles, +38 %)
+  auto gl = [&](int kt_, int j, int gk_) -> bool {
+    if (!GRR) return false;
+    const int t0 = kt_ + j - LA;
+    if (t0 < 0 || t0 + kpg >= kt_count) return false;
+    int r = gk_ + j - LA;
+    while (r < 0) r += kpg;
+    return r == 0;
+  };
+  auto gload = [&](int gi) {   // GRR: this lane's columns of group gi into graw_s / graw_z (no wait)
+#pragma unroll
+    for (int t = 0; t < TN; ++t)
+#pragma unroll
+      for (int h = 0; h < (M16 ? 2 : 1); ++h) {
+        const int c = n0 + wn * WN + (M16 ? 32 * t + 16 * h + (lane & 15) : 32 * t + (lane & 31));
+        const _Float16* sp = scales + (int64_t)gi * N + c;
+        const uint32_t* zp = qzeros + (int64_t)gi * (N / 8) + (c >> 3);
+        asm volatile("global_load_ushort %0, %1, off" : "+v"(graw_s[t][h]) : "v"(sp));
+        asm volatile("global_load_dword %0, %1, off" : "+v"(graw_z[t][h]) : "v"(zp));
+      }
+  };
 
   int col[TN];
   W4Zero zc[TN];
@@ -1522,6 +1558,7 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   if ((VAR & 256) && grp) __builtin_amdgcn_s_setprio(1);
   // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
   const int pro = kt_count < LA ? kt_count : LA;
+  if (GRR) gload(0);   // older than every piece: the prologue's retire wait for tile 0 covers it
 #pragma unroll
   for (int j = 0; j < LA; ++j)
     if (j < pro) issue(j, j, 0, NPW);
@@ -1532,7 +1569,7 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
     vm_wait_le<(LA - 1) * NPW>(newer);
   }
   __builtin_amdgcn_s_barrier();
-  if (GR && !G_NOROW) gread(0);   // tile 0's row: wave 0's retire wait precedes the barrier above
+  if (GROW && !G_NOROW) gread(0);   // tile 0's row: wave 0's retire wait precedes the barrier above
   if (grp) __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
@@ -1545,6 +1582,7 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
   };
   int slot = 0;
   int gk = 0;   // GR: K tiles since the current group's first
+  int gidx = 0; // GR: the current group
   for (int kt = 0; kt < kt_count; ++kt) {
     const char* st = smem + slot * STAGE;
     const int ahead = kt + LA;
@@ -1561,14 +1599,41 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
         // the runtime form is a ~40-SALU / 15-branch decision tree on the load half's stream
         if (!GR && pf && kt + LA < kt_count) {
           vm_wait<(LA - 2) * NPW + PRE_LAST>();
+        } else if (GRR && LA == 3 && NPH > 1 && kpg == 2 && pf && kt + LA < kt_count) {
+          // GRR, two K tiles per group (G = 128): of the two tiles kt - 1, kt exactly one starts a
+          // group, so one set of register-row loads is newer -- a constant count, no decision tree
+          vm_wait<(LA - 2) * NPW + PRE_LAST + NGL>();
         } else {
           int newer = pf ? PRE_LAST : 0;
+          if (NPH > 1 && GRR && gk == 0 && kt + kpg < kt_count) newer += NGL;   // gl(ahead)   // this tile's register-row loads (phase 0)
 #pragma unroll
-          for (int j = 2; j < LA; ++j) newer += kt + j < kt_count ? npieces(kt + j) : 0;
-          vm_wait_le<(LA - 2) * NPW + PRE_LAST>(newer);
+          for (int j = 2; j < LA; ++j) newer += (kt + j < kt_count ? npieces(kt + j) : 0) + (gl(kt, j, gk) ? NGL : 0);
+          vm_wait_le<(LA - 2) * (NPW + NGL) + PRE_LAST + NGL>(newer);
         }
       }
       if (GR && !G_NOROW && p == 0 && gk == 0) {   // first K tile of a group: its scale / zero splats
+        if constexpr (GRR) {
+          // the group's loads were issued kpg tiles ago, before the pieces of tiles kt - kpg + LA ..
+          // kt + LA - 1 (those that exist); everything older has retired once at most that many
+          // remain.  (kt == 0: the prologue's wait covered them.)  The empty asm re-defines the
+          // registers after the wait, so nothing reading them is scheduled above it.
+          if (kt > 0) {
+            int left = kt_count - (kt - kpg + LA);
+            left = (VAR & 1) || left < 0 ? 0 : left > kpg ? kpg : left;
+            if (kpg == 2 && left == 2)
+              vm_wait<2 * NPW>();
+            else
+              vm_wait_le<3 * NPW>(left * NPW);
+          }
+#pragma unroll
+          for (int t = 0; t < TN; ++t)
+#pragma unroll
+            for (int h = 0; h < (M16 ? 2 : 1); ++h) {
+              asm volatile("" : "+v"(graw_s[t][h]), "+v"(graw_z[t][h]));
+              graw_s[t][h] &= 0xFFFFu;
+              graw_z[t][h] >>= 4 * ((n0 + wn * WN + (M16 ? 32 * t + 16 * h + (lane & 15) : 32 * t + (lane & 31))) & 7);
+            }
+        }
 #pragma unroll
         for (int t = 0; t < TN; ++t)
 #pragma unroll
@@ -1689,10 +1754,12 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
       }
       // the next-next tile's LDS-DMA pieces behind this MFMA burst (the wave would only wait at
       // the barrier otherwise; WAR-safe in every phase: see header)
+      // GRR: the next group's register rows, older than tile ahead's pieces (gl(ahead))
+      if (GRR && p == 0 && gk == 0 && kt + kpg < kt_count) gload(gidx + 1);   // == gl(ahead)
       if (pf && !DMA_LOAD && !DMA_SPREAD) issue(ahead, sa, pp2_pre(p, NPW, NPH, 0), pp2_pre(p + 1, NPW, NPH, 0));
       // GR: tile kt+1 starts a group -> its row into registers (every wave's retire wait for tile
       // kt+1, wave 0's included, precedes the barrier that opened this MFMA half)
-      if (GR && !G_NOROW && p == NPH - 1 && kt + 1 < kt_count && gk + 1 == kpg)
+      if (GROW && !G_NOROW && p == NPH - 1 && kt + 1 < kt_count && gk + 1 == kpg)
         gread(slot + 1 == STAGES ? 0 : slot + 1);
       if (VAR & 4) stamp(2);
       if (!(VAR & 256)) __builtin_amdgcn_s_setprio(0);
@@ -1702,7 +1769,10 @@ void pp2_tile(const _Float16* __restrict__ A, int64_t lda, const u32x4* __restri
       if (VAR & 4) stamp(3);
     });
     slot = slot == STAGES - 1 ? 0 : slot + 1;
-    if (GR) gk = gk + 1 == kpg ? 0 : gk + 1;
+    if (GR) {
+      gidx += gk + 1 == kpg ? 1 : 0;
+      gk = gk + 1 == kpg ? 0 : gk + 1;
+    }
   }
   if (!grp) __builtin_amdgcn_s_barrier();   // balance group 1's extra barrier
   if ((VAR & 4) && lane == 0) {
@@ -1930,9 +2000,17 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
   if (cfg >= 50 && cfg < 200) {   // ping-pong kernels
     if (GR) {   // grouped weights: the per-group scale / zero row rides in the ring (VAR & 512)
       switch (cfg) {
-        // 3 slots, lookahead 2: four 40 KiB stages fill the 160 KiB LDS, the group row needs 640 B more
-        case 57: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
+        // the group's scale / zero words prefetched into VGPRs (VAR & (1 << 23)): 4 slots, lookahead 3
+        case 57: case 112: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 4096 | (1 << 23)>(a, st);
+        // the group row in the ring: 3 slots, lookahead 2 (four 40 KiB stages fill the 160 KiB LDS,
+        // the group row needs 640 B more)
+        case 114: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
         case 64: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16>(a, st);   // (slower than 57 on every shape)
+        // register rows (VAR & (1 << 23)): no group row in the ring -> 4 slots / lookahead 3
+        case 113: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 16 | 4096 | (1 << 23)>(a, st);
+#ifdef SAMQ_TUNING
+        case 116: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 4096 | (1 << 23) | 1024>(a, st);   // timing-only: no group scaling
+#endif
         default: return fail(SAMQ_ERR_INVALID, "w4a16_gemm: grouped weights take ping-pong configs 57 / 64 only");
       }
     }
@@ -1941,10 +2019,10 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
       case 56: return launch_pp2<2, 4, 2, 2, 4, 2, EPI>(a, st);   // 4 slots, lookahead 2 (DMA in both phases)
       // 4 slots, lookahead 3; the wave index in an SGPR (VAR & 4096: uniform piece addressing,
       // -3..-6 % isolated vs the VGPR form at M = 8192, profiles/r3_gemm_rfl.log)
-      case 57: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);
+      case 57: case 112: case 114: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096>(a, st);   // (112-114: grouped forms)
       case 58: return launch_pp2<2, 4, 2, 1, 4, 2, EPI>(a, st);   // 1 phase / K tile, 4 slots, lookahead 2
       case 62: return launch_pp2<4, 2, 4, 2, 4, 3, EPI>(a, st);   // 4x2 waves (64x128 each): A read 2x, B 4x
-      case 64: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);  // cfg 57 on 16x16x32 MFMA
+      case 64: case 113: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 16 | 4096>(a, st);  // cfg 57 on 16x16x32 MFMA
       case 65: return launch_pp2<2, 4, 2, 2, 4, 2, EPI, 16>(a, st);  // cfg 56 on 16x16x32 MFMA
       // cfg 57 / 64 with the LDS-DMA pieces spread through the MFMA burst (VAR & 16384)
       case 100: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 4096 | 16384>(a, st);
@@ -2109,7 +2187,7 @@ static int cfg_bn(int cfg) {
                  case 74: case 75: case 76: case 77: case 78: case 79: return 256;
                  case 90: case 91: case 92: case 93: case 94: case 95: case 96: return 256;
                  case 97: case 98: return 512;
-                 case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109: case 110: case 111: return 256;
+                 case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109: case 110: case 111: case 112: case 113: case 114: case 115: case 116: return 256;
                  default: return 0; }
 }
 

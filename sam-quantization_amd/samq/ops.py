@@ -23,7 +23,7 @@ EPI_BIAS_LNF = _lib.EPI_BIAS_LNF
 EPI_GELU_LNF = _lib.EPI_GELU_LNF
 
 # W4A16 tile configs of the product library (include/samq.h, samq_w4a16_gemm_cfg); 0 = automatic
-W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65, 100, 101, 104, 107, 108, 109, 110, 111))
+W4A16_CFGS = frozenset((1, 2, 3, 4, 5, 6, 7, 9, 21, 22, 23, 24, 25, 26, 29, 30, 31, 55, 56, 57, 58, 62, 64, 65, 100, 101, 104, 107, 108, 109, 110, 111, 112, 113, 114))
 _Q8_EPIS = (EPI_Q8, EPI_Q8_GELU, EPI_Q8_RES)
 
 

@@ -150,7 +150,7 @@ def test_w4a16_gemm_persistent_matches(cuda, cfg, base, epi):
         assert torch.equal(o1, o2), (m, k, n)
 
 
-@pytest.mark.parametrize("cfg", [57, 64])
+@pytest.mark.parametrize("cfg", [57, 64, 114])
 @pytest.mark.parametrize("groupsize", [64, 128, 256])
 @pytest.mark.parametrize("epi", ["bias", "gelu", "resadd", "f32"])
 def test_w4a16_gemm_pingpong_grouped(cuda, cfg, groupsize, epi):
@@ -164,6 +164,39 @@ def test_w4a16_gemm_pingpong_grouped(cuda, cfg, groupsize, epi):
         a = rng.standard_normal((m, k), dtype=np.float32).astype(np.float16)
         y = gptq_pack.matmul4_g1(a, qw, sc, qz, groupsize, bias)
         _epi_check(ops, cuda, a, y, ops.w4_repack(_dev(qw, cuda)), sc, qz, bias, n, groupsize, epi, cfg, rng)
+
+
+@pytest.mark.parametrize("cfg,base", [(112, 114), (113, 64)])
+@pytest.mark.parametrize("groupsize", [64, 128, 192, 256])
+def test_w4a16_grouped_register_rows(cuda, cfg, base, groupsize):
+    """Grouped ping-pong with register rows (the group's scale / zero words loaded into VGPRs ahead
+    of the group, counted in the ring's vmcnt; 4 ring slots; cfg 112 = the grouped cfg 57) against
+    the ring-row form (cfg 114, the group row as one more LDS-DMA piece per stage): identical
+    bits (same unpack, same MFMA order) for 1 .. 80 K tiles, 1 .. 4 K tiles per group, every
+    epilogue, plus the oracle at the largest K."""
+    from samq import ops
+    shapes = [(300, 64 * t, 256) for t in (1, 2, 3, 4, 5, 7)] + [(333, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280)]
+    for m, k, n in shapes:
+        if k % groupsize:
+            continue
+        qw, qz, sc, bias = _packed_layer(k, n, groupsize, seed=k + groupsize + cfg)
+        g = torch.Generator(device=cuda).manual_seed(k + groupsize)
+        a = torch.randn((m, k), generator=g, device=cuda).half()
+        packed = ops.w4_repack(_dev(qw, cuda))
+        args = (a, packed, _dev(sc, cuda), _dev(qz, cuda), _dev(bias, cuda), n, groupsize)
+        for e in (ops.EPI_BIAS, ops.EPI_BIAS_GELU, ops.EPI_RESADD_F32, ops.EPI_F32):
+            if e == ops.EPI_RESADD_F32:
+                r0 = torch.randn((m, n), generator=g, device=cuda)
+                o1, o2 = r0.clone(), r0.clone()
+                ops.w4a16_gemm(*args, e, out=o1, cfg=base)
+                ops.w4a16_gemm(*args, e, out=o2, cfg=cfg)
+            else:
+                o1 = ops.w4a16_gemm(*args, e, cfg=base)
+                o2 = ops.w4a16_gemm(*args, e, cfg=cfg)
+            torch.cuda.synchronize()
+            assert torch.equal(o1, o2), (m, k, n, e)
+    y = gptq_pack.matmul4_g1(a.cpu().numpy(), qw, sc, qz, groupsize, bias)
+    _close(ops.w4a16_gemm(*args, ops.EPI_BIAS, cfg=cfg), y, 4e-3)
 
 
 @pytest.mark.parametrize("groupsize", [-1, 128])

@@ -20,9 +20,11 @@
 #   pmci8                  int8 GEMM counters (tools/pmc_i8.sh)
 #   i8=<cfgs>@<m>          int8 GEMM tile configs (tools/bench_i8.py, tuning library)
 #   w4=<cfgs>@<m>          W4A16 GEMM tile configs (tools/bench_gemm.py, tuning library)
+#   w4g=<cfgs>@<m>         the same with G = 128 grouped weights
 #   ab48=<variants>        in-graph W4A8 per-layer cfg A/B (tools/bench_cfg_ab_w4a8.py, tuning library)
 #   ab16=<variants>        in-graph W4A16 per-layer cfg A/B (tools/bench_cfg_ab.py, tuning library)
 #   abl=<mode>@<lib.so>    bench <mode> alternating this build and <lib.so> (SAMQ_LIB), 2 rounds each
+#   ablg=<lib.so>          W4A16 G = 128 bench alternating this build and <lib.so>, 3 rounds each
 #   lanes=<mode>@<l1,l2..> bench <mode> at each lane count (2 rounds each, alternating)
 #   attn                   attention kernels isolated (tools/bench_attn.py)
 #   attnq8                 W8A8 attention kernels isolated (tools/bench_attn_q8.py)
@@ -98,6 +100,8 @@ PY
                 --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 ;;
     w4=*)     run w4_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_gemm.py \
                 --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 ;;
+    w4g=*)    run w4g_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_gemm.py \
+                --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 --groupsize 128 ;;
     ab48=*)   run ab48 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab_w4a8.py 2 6 "$arg" ;;
     ab16=*)   run ab16 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab.py 2 6 "$arg" ;;
     abl=*)    m=${arg%@*}; lib=${arg#*@}
@@ -106,6 +110,13 @@ PY
                 run abl_${m}_lib_$r 400 env SAMQ_LIB="$lib" python bench.py --mode "$m" --steps 10 --warmup 3 --no-cpu-baseline --no-isolated
               done
               for f in gpurun_out/$tag.abl_${m}_*.log; do
+                echo "$f $(grep -h '"value"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
+              done ;;
+    ablg=*)   for r in 1 2 3; do
+                run ablg_new_$r 400 python bench.py --groupsize 128 --steps 10 --warmup 3 --no-cpu-baseline --no-isolated --no-modes
+                run ablg_lib_$r 400 env SAMQ_LIB="$arg" python bench.py --groupsize 128 --steps 10 --warmup 3 --no-cpu-baseline --no-isolated --no-modes
+              done
+              for f in gpurun_out/$tag.ablg_*.log; do
                 echo "$f $(grep -h '"value"' "$f" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")"
               done ;;
     lanes=*)  m=${arg%@*}; ls=${arg#*@}
