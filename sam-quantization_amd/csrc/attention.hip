@@ -1531,9 +1531,7 @@ template <int D>
 static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   const int items = units * p.heads;
 #ifdef SAMQ_TUNING
-  // tuning A/B: 2 = the round-3 scaled-Q form (Win !UNSC); 4 = the int8 store with P as hi + lo
-  // (PHL: W4A8 window-stage codes off by one 1.2-1.3e-3 vs 2.1-2.2e-3, but the int8-store launch
-  // 45.4 vs 35.5 us and the W4A8 step 35.7 vs 35.1 ms, profiles/r4_o.*: not the product path)
+  // tuning A/B: 2 = the round-3 scaled-Q form (Win !UNSC); 4 = hi + lo P for either output
   const char* e = getenv("SAMQ_ATTN_WIN");
   if (e && (atoi(e) == 2 || atoi(e) == 4)) {
     if (atoi(e) == 2) hipLaunchKernelGGL((win_attention_kernel<D, false>), dim3(items), dim3(256), 0, stream, p, items);
@@ -1543,8 +1541,15 @@ static int launch_win(const AttnParams& p, int units, hipStream_t stream) {
   }
 #endif
   // unscaled Q (UNSC): 35.6 vs 36.2 us per ViT-H 2-image launch, fp16 output 1.59e-3 vs 1.95e-3
-  // max-abs from the fp32 oracle, W4A8 store codes off by one 1.7e-3 vs 2.5e-3 (profiles/r4_m.win.log)
-  hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
+  // max-abs from the fp32 oracle, W4A8 store codes off by one 1.7e-3 vs 2.5e-3 (profiles/r4_m.win.log).
+  // The W4A8 int8-code store (round 5): P as fp16 hi + lo (PHL), the output at
+  // fp32-level error before the proj QAct's quantiser -- window-stage codes off by one 1.21-1.33e-3
+  // instead of 2.05-2.24e-3, for two MFMAs per P.V step (int8-store launch 45.4 vs 35.5 us, W4A8
+  // step -1.4 %, profiles/r5_w4a8_window_phl.log)
+  if (p.out_scale > 0.f)
+    hipLaunchKernelGGL((win_attention_kernel<D, true, true>), dim3(items), dim3(256), 0, stream, p, items);
+  else
+    hipLaunchKernelGGL((win_attention_kernel<D, true>), dim3(items), dim3(256), 0, stream, p, items);
   SAMQ_LAUNCH_CHECK("win_attention launch");
   return SAMQ_OK;
 }

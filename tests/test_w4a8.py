@@ -214,10 +214,12 @@ def _float_close(out, ref, rtol, atol_frac, what):
 # fp16-arithmetic attention (fp16 Q/K/V/P on the MFMA, fp32 softmax) against the oracle's fp32
 # attention.  Measured (ViT-H, 1024^2): round 3, quantising the fp16-rounded output, 3.7e-3
 # (window) / 5.3e-3 (global); round 4, quantising the f32 output (attn_store4), 2.7-3.0e-3 (window)
-# / 0.93-0.98e-3 (global), per-channel and G = 128 -- bound 5e-3; the integer-exact stages
-# measured 0 .. 4e-6
+# / 0.93-0.98e-3 (global), per-channel and G = 128; round 5, the window kernel's int8 store with P
+# as fp16 hi + lo (PHL; W4A8 step -1.4 %, profiles/r5_w4a8_window_phl.log),
+# 1.21-1.33e-3 (window) / 0.93-0.98e-3 (global) -- bound: the largest measured + 20 %; the
+# integer-exact stages measured 0 .. 4e-6
 W4A8_EXACT_FRAC = 1e-4
-W4A8_ATTN_FRAC = 5e-3
+W4A8_ATTN_FRAC = 1.6e-3
 
 
 @pytest.mark.gpu
