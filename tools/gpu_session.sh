@@ -17,7 +17,7 @@
 #                          profiles/, so later bench steps in the same call quote them; copies of
 #                          them come back in gpurun_out/publish_<round>/ (raw trace dirs removed)
 #   attnpmc                attention counters (tools/attn_pmc.sh)
-#   pmci8                  int8 GEMM counters (tools/pmc_i8.sh)
+#   pmci8[=<cfgs>]         int8 GEMM counters (tools/pmc_i8.sh; default cfgs 86,94)
 #   i8=<cfgs>@<m>          int8 GEMM tile configs (tools/bench_i8.py, tuning library)
 #   w4=<cfgs>@<m>          W4A16 GEMM tile configs (tools/bench_gemm.py, tuning library)
 #   w4g=<cfgs>@<m>         the same with G = 128 grouped weights
@@ -96,6 +96,7 @@ PY
               ls -l gpurun_out/publish_"$arg" ;;
     attnpmc)  run attnpmc 400 bash tools/attn_pmc.sh ;;
     pmci8)    run pmci8 400 bash tools/pmc_i8.sh ;;
+    pmci8=*)  run pmci8_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 bash tools/pmc_i8.sh "$arg" ;;
     i8=*)     run i8_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_i8.py \
                 --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 ;;
     w4=*)     run w4_$(echo "$arg" | tr -c 'a-zA-Z0-9' '_') 400 env SAMQ_LIB=tuning python -u tools/bench_gemm.py \
