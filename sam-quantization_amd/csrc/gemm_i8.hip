@@ -545,9 +545,6 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   const int grp = wave >> 2;
   const int tiles_n = N / BN;
   const int tiles_m = (M + BM - 1) / BM;
-  // (round 5: an XCD column raster -- each XCD walking its eighth of the tiles column by column --
-  // cut lin1's L2 fetch 161 -> 123 MB but ran 1-2 % slower in the W4A8 graph,
-  // profiles/r5_i8_xcd_raster.log)
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int m0 = (bid / tiles_n) * BM;
   const int n0 = (bid % tiles_n) * BN;
@@ -1046,7 +1043,6 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 93:   // cfg 86 with the LDS-DMA pieces spread through the MFMA bursts
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 93 is the W4 ping-pong kernel");
-
 #ifdef SAMQ_TUNING
     case 99:   // tile ping-pong: one group's epilogue under the other group's main loop (correct, slower)
       if constexpr (BF == BF_W4) return launch_i8_tpp<EPI>(a, st);
