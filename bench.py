@@ -734,7 +734,9 @@ def main():
     if args.dry_run:
         return dry_run(args, rank, world)
 
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    # one GPU per local rank; more ranks than GPUs (a gloo rehearsal of the N-rank path on a smaller
+    # box) share them round-robin
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     mode = args.mode
     batch = args.batch or default_batch(mode, world)
