@@ -758,7 +758,11 @@ def main():
         torch.cuda.empty_cache()
         for m in ("w4a8", "w8a8"):
             b = default_batch(m, world)
-            modes[m] = run_mode(m, args, rank, world, dev, b, default_lanes(m, b), headline=False)
+            try:   # a sub-mode failure is reported in the line; it never costs the headline record
+                modes[m] = run_mode(m, args, rank, world, dev, b, default_lanes(m, b), headline=False)
+            except Exception as e:  # noqa: BLE001
+                log(f"mode {m} failed: {type(e).__name__}: {e}")
+                modes[m] = {"error": f"{type(e).__name__}: {e}"}
             torch.cuda.empty_cache()
     if rank == 0:
         line = {"metric": METRIC, "value": rec.pop("value"), "unit": rec.pop("unit"), "n_gpus": world,
