@@ -1100,6 +1100,10 @@ static int i8_pick_cfg(int M, int N, int bfmt) {
   // Round 3: on a 2-stage ring (32 KiB LDS, five workgroups per CU instead of three) the W8A8
   // graph takes 1.8325 vs 1.8610 ms per image, bit-identical; 128x64 / 64x128 tiles were slower
   // (tools/bench_cfg_ab_w8a8.py, profiles/r3_w8_cfg_ab.log).
+  // Round 5: the wide outputs (qkv N = 2304, lin1 N = 3072 at vit_b) on 64x128 tiles, 2 stages
+  // (cfg 90): in the W8A8 graph 1.7067 vs 1.7568 ms per image, bit-identical; proj / lin2 (N = 768)
+  // stay on 64x64 (all four on 64x128: 1.7335; profiles/r5_w8_cfg_ab_64x128.log)
+  if (bfmt == BF_W8 && t256 < 512 && N % 128 == 0 && N > 1024) return 90;
   if (bfmt == BF_W8 && t256 < 512 && N % 64 == 0) return 89;
   if (N % 256 == 0 && t256 >= 512) return 82;
   if (N % 128 == 0 && M >= 256) return 83;
