@@ -210,7 +210,7 @@ class EncoderEngine:
             ops.add_layernorm(x, self._delta(bufs, torch.float32), p.ln1_w, p.ln1_b, p.ln1_eps, out=xn8,
                               out_scale=p.s_qkv)
         else:
-            ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8)
+            ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8, rows_per_wave=self.ln_rpw)
         mark(0)
         p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
         mark(1)
@@ -226,7 +226,7 @@ class EncoderEngine:
         else:
             p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
             mark(3)
-            ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8)
+            ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8, rows_per_wave=self.ln_rpw)
         mark(4)
         p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
         mark(5)

@@ -698,6 +698,10 @@ class W8A8Engine:
         if not (cfg.BIT_TYPE_A.signed and cfg.BIT_TYPE_A.bits == 8) or cfg.INT_NORM or cfg.INT_SOFTMAX:
             raise NotImplementedError("W8A8 engine supports Config(ptf=False, lis=False) with BIT_TYPE_A=int8")
         self.enc = enc
+        # LayerNorm-q rows per wave: one (1024 workgroups for the 4096 vit_b rows instead of 512) --
+        # in the W8A8 graph 1.6543 vs 1.6836 ms per image, bit-identical; the ViT-H W4A8 graph keeps
+        # the library default (two: -2.2 % with one, profiles/r5_ln_rpw_ab.log)
+        self.ln_rpw = 1
         dev = enc.pos_embed.device
         if dev.type != "cuda":
             raise RuntimeError("W8A8 engine: move the encoder to the GPU first")
@@ -792,7 +796,7 @@ class W8A8Engine:
         for i, bl in enumerate(self.blocks):
             pre = f"blocks.{i}."
             g1, b1, e1 = bl["n1"]
-            ops.layernorm_q(x, g1, b1, e1, in_scale=s_x, out_scale=bl["s_ln1"], out=xn)
+            ops.layernorm_q(x, g1, b1, e1, in_scale=s_x, out_scale=bl["s_ln1"], out=xn, rows_per_wave=self.ln_rpw)
             tap(pre + "qact1", xn.view(b, gh, gw, c), bl["s_ln1"])
             qkv = self._gemm(xn, bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"]).view(b, gh, gw, 3 * c)
             tap(pre + "attn.qact1", qkv, bl["s_qkv"])
@@ -804,7 +808,7 @@ class W8A8Engine:
                        out=x)
             tap(pre + "qact2", x.view(b, gh, gw, c), bl["s_x1"])
             g2, b2, e2 = bl["n2"]
-            ops.layernorm_q(x, g2, b2, e2, in_scale=bl["s_x1"], out_scale=bl["s_ln2"], out=xn)
+            ops.layernorm_q(x, g2, b2, e2, in_scale=bl["s_x1"], out_scale=bl["s_ln2"], out=xn, rows_per_wave=self.ln_rpw)
             tap(pre + "qact3", xn.view(b, gh, gw, c), bl["s_ln2"])
             hbuf = self._gemm(xn, bl["lin1"], ops.EPI_Q8_GELU, bl["s_ln2"], bl["s_h"])
             tap(pre + "mlp.qact1", hbuf.view(b, gh, gw, -1), bl["s_h"])

@@ -350,9 +350,10 @@ def minmax_update(x2d: torch.Tensor, axis: int, max_val: Optional[torch.Tensor] 
 
 def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, in_scale: float = 0.0,
                 out_scale: float = 0.0, out_dtype: torch.dtype = torch.int8,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, rows_per_wave: int = 0) -> torch.Tensor:
     """LayerNorm with int8 codes on either side: x int8 (codes * in_scale) / f32 / f16;
-    out int8 codes (q(y, out_scale)), f32 fake-quant (out_dtype f32 with out_scale > 0), f16 or f32."""
+    out int8 codes (q(y, out_scale)), f32 fake-quant (out_dtype f32 with out_scale > 0), f16 or f32.
+    ``rows_per_wave`` (1, 2, 4; 0 = library default) as in ``layernorm``."""
     _need_cuda(x, gamma, beta)
     c = x.shape[-1]
     assert x.is_contiguous() and gamma.dtype == torch.float32 and beta.dtype == torch.float32
@@ -367,6 +368,7 @@ def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: f
         flags |= _lib.LN_OUT_I8
     elif out.dtype == torch.float32:
         flags |= _lib.LN_OUT_F32 | (_lib.LN_OUT_I8 if out_scale > 0 else 0)
+    flags |= rows_per_wave << 16
     _lib.check(_lib.load().samq_layernorm_q(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), x.numel() // c, c,
                                             float(eps), flags, float(in_scale), float(out_scale), _stream()),
                "layernorm_q")

@@ -34,6 +34,7 @@ img = torch.randn((8, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.res_mode = cfg.get("res", "epi")
+    eng.ln_rpw = cfg.get("ln_rpw", 0)
     eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):

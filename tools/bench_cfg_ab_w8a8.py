@@ -27,6 +27,7 @@ g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((1, 3, 1024, 1024), generator=g, device=dev)
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
+    eng.ln_rpw = cfg.get("ln_rpw", 0)
     for bl in eng.blocks:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             bl[lay]["cfg"] = cfg.get(lay, 0)
