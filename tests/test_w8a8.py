@@ -276,6 +276,12 @@ def test_quantize_and_layernorm_q(cuda):
                                torch.from_numpy(b).to(cuda), eps, in_scale=float(s), out_scale=float(s_o),
                                out_dtype=torch.float32).cpu().numpy()
         np.testing.assert_array_equal(fq32, out.cpu().numpy().astype(np.float32) * s_o)
+        # rows per wave (the W8A8 engine runs one): same codes, including the ragged last wave
+        for rpw in (1, 2, 4):
+            o2 = ops.layernorm_q(torch.from_numpy(xc).to(cuda), torch.from_numpy(g).to(cuda),
+                                 torch.from_numpy(b).to(cuda), eps, in_scale=float(s), out_scale=float(s_o),
+                                 rows_per_wave=rpw)
+            assert torch.equal(o2.cpu(), out.cpu()), rpw
 
 
 def _attn_ref(qkv_codes, bias, relh, relw, heads, window, s_qkv, s1, s2, s_o):
