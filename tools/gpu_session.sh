@@ -24,7 +24,7 @@
 #   ab48=<variants>        in-graph W4A8 per-layer cfg A/B (tools/bench_cfg_ab_w4a8.py, tuning library)
 #   ab16=<variants>        in-graph W4A16 per-layer cfg A/B (tools/bench_cfg_ab.py, tuning library)
 #   ab16g=<variants>       the same with G = 128 grouped weights (product library)
-#   ab88=<variants>        in-graph W8A8 per-layer cfg A/B (tools/bench_cfg_ab_w8a8.py)
+#   ab88=<variants>        in-graph W8A8 per-layer cfg A/B (tools/bench_cfg_ab_w8a8.py, tuning library)
 #   abl=<mode>@<lib.so>    bench <mode> alternating this build and <lib.so> (SAMQ_LIB), 2 rounds each
 #   ablg=<lib.so>          W4A16 G = 128 bench alternating this build and <lib.so>, 3 rounds each
 #   lanes=<mode>@<l1,l2..> bench <mode> at each lane count (2 rounds each, alternating)
@@ -107,7 +107,7 @@ PY
                 --cfgs "${arg%@*}" --m "${arg#*@}" --iters 10 --groupsize 128 ;;
     ab48=*)   run ab48 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab_w4a8.py 2 6 "$arg" ;;
     ab16g=*)  run ab16g 500 env SAMQ_AB_GS=128 python -u tools/bench_cfg_ab.py 2 6 "$arg" ;;
-    ab88=*)   run ab88 500 python -u tools/bench_cfg_ab_w8a8.py 10 "$arg" ;;
+    ab88=*)   run ab88 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab_w8a8.py 10 "$arg" ;;
     ab16=*)   run ab16 500 env SAMQ_LIB=tuning python -u tools/bench_cfg_ab.py 2 6 "$arg" ;;
     abl=*)    m=${arg%@*}; lib=${arg#*@}
               for r in 1 2; do
