@@ -187,6 +187,8 @@ class EncoderEngine:
         same kernel (``Sam.preprocess`` fused, ``samq_patch_embed_u8``)."""
         p = self.patch
         pos = None if self.pos is None else self.pos[0]
+        if "embed" in self.skip:   # timing-only (in-graph A/B): no patch embedding
+            return
         if img.dtype == torch.uint8:
             if self._pixel_norm is None:
                 raise ValueError("uint8 pixels need pixel_norm=(pixel_mean, pixel_std)")
@@ -345,6 +347,8 @@ class EncoderEngine:
         """Neck (image_encoder.py:88-104) on NHWC tokens: 1x1 conv (HIP, fp32 tokens -> fp16),
         LayerNorm2d (HIP), 3x3 conv (HIP implicit GEMM, zero padding in the gather), LayerNorm2d."""
         b, g = x32.shape[0], self.grid
+        if "neck" in self.skip:   # timing-only (in-graph A/B): no neck
+            return torch.empty((b, self.n0_w.shape[0], g, g), dtype=out_dtype or torch.float16, device=x32.device)
         y = ops.conv1x1_f32(x32, self.n0_w)                                                # (b, g, g, oc) f16
         y = ops.layernorm(y, *self.n1[:2], eps=self.n1[2])                                 # LN2d (NHWC rows)
         y = ops.conv3x3_nhwc(y, self.n2_w_tap)                                             # 3x3, pad 1
