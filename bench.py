@@ -303,21 +303,27 @@ def oracle_state(enc, cfg, groupsize: int):
     return st, lw, lb, np
 
 
-def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, groupsize: int = -1, runs: int = 3):
-    """Oracle restatement of the reference CPU fake-quant path on one 1024x1024 image, rank 0 only.
-    With the bench encoder (``enc``) and its image 0 (``img0``) the oracle is built from the
-    encoder's OWN weights -- W4A16 / W4A8: its packed int4 buffers dequantised (G1) plus, for W4A8,
-    its calibrated activation scales; W8A8: its fp32 weights and calibrated QAct scales -- so its
-    output doubles as the parity reference (returned second).  ``runs`` = 3: median of 3 after one
-    warm-up; ``runs`` = 1 (the sub-mode records): one cold run, the parity reference itself."""
+def _cpu_threads(parity_only: bool = False) -> int:
+    """Host threads for the oracle: the box's grant (affinity, capped by OMP_NUM_THREADS).  The
+    parity-only leg of an N > 1 run (the other ranks idle at a barrier meanwhile) ignores an
+    OMP_NUM_THREADS of 1 set by a launcher, up to 16 threads."""
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", aff))
+    return max(min(aff, omp), min(aff, 16)) if parity_only else min(aff, omp)
+
+
+def build_oracle(model_name: str, mode: str, enc=None, groupsize: int = -1, precision: str = "fp32"):
+    """The mode's oracle (checker side): with the bench encoder ``enc`` it is built from the
+    encoder's OWN weights -- W4A16 / W4A8: its packed int4 buffers dequantised (G1) plus, for
+    W4A8, its calibrated activation scales; W8A8: its fp32 weights and calibrated QAct scales --
+    else from seeded random weights.  ``precision`` "fp64" evaluates the same fake-quant graph in
+    float64 (the int8 modes' self-distance reference point).  Returns (oracle, description)."""
     sys.path.insert(0, str(REPO))
     from oracle import sam_ref, synth
-    threads = len(os.sched_getaffinity(0))
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
-    torch.set_num_threads(threads)
     cfg = synth.encoder_config(model_name)
     g = torch.Generator().manual_seed(0)
-    own = enc is not None and img0 is not None
+    own = enc is not None
+    dt = {"fp32": torch.float32, "fp64": torch.float64}[precision]
     if mode == "w8a8":
         from oracle import fq_ref
         from samq import fq_vit
@@ -328,7 +334,7 @@ def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, grou
         else:
             st = {k: torch.randn(shape, generator=g) * 0.02 for k, shape in _state_shapes(cfg).items()}
             scales = None
-        o = fq_ref.FQEncoderOracle(cfg, st)
+        o = fq_ref.FQEncoderOracle(cfg, st, dtype=dt)
         if scales is None:
             qa = ["qact_input", "patch_embed.qact", "qact_pos", "qact1"] + [f"qacts.{i}" for i in range(4)]
             for i in range(cfg["depth"]):
@@ -337,30 +343,43 @@ def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, grou
                                                      "mlp.qact1", "mlp.qact2")]
             scales = {n: 0.05 for n in qa}
         o.set_scales(scales)
-        what = "fq_vit W8A8 fake-quant op graph (oracle/fq_ref.py)"
+        return o, "fq_vit W8A8 fake-quant op graph (oracle/fq_ref.py)"
+    lw = lb = None
+    if own:
+        st, lw, lb, _ = oracle_state(enc, cfg, groupsize)
     else:
+        st = {k: torch.randn(shape, generator=g) * 0.02 for k, shape in _state_shapes(cfg).items()}
+    if mode == "w4a8":
+        from oracle import w4a8_ref
+        o = w4a8_ref.W4A8EncoderOracle(cfg, st, precision=precision, linear_weights=lw, linear_bias=lb)
         if own:
-            st, lw, lb, _ = oracle_state(enc, cfg, groupsize)
+            from samq import QuantLinear
+            o.set_scales({n.replace("qkv_proj", "qkv").replace("o_proj", "proj"): float(m.act_quant.quantizer.scale)
+                          for n, m in enc.named_modules() if isinstance(m, QuantLinear)})
         else:
-            st = {k: torch.randn(shape, generator=g) * 0.02 for k, shape in _state_shapes(cfg).items()}
-        if mode == "w4a8":
-            from oracle import w4a8_ref
-            if own:
-                from samq import QuantLinear
-                o = w4a8_ref.W4A8EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb)
-                o.set_scales({n.replace("qkv_proj", "qkv").replace("o_proj", "proj"): float(m.act_quant.quantizer.scale)
-                              for n, m in enc.named_modules() if isinstance(m, QuantLinear)})
-            else:
-                o = w4a8_ref.W4A8EncoderOracle(cfg, st)
-                o.set_scales({n: 0.05 for n in synth.linear_names(cfg)})
-            what = "W4A8 fake-quant op graph (oracle/w4a8_ref.py)"
-        else:
-            o = sam_ref.EncoderOracle(cfg, st, linear_weights=lw, linear_bias=lb) if own else \
-                sam_ref.EncoderOracle(cfg, st)
-            what = "fp32 CPU fake-quant op graph (oracle/sam_ref.py)"
-    img = img0.detach().float().cpu().reshape(1, 3, 1024, 1024) if own else torch.randn(1, 3, 1024, 1024, generator=g)
-    if runs > 1:
-        o(img)   # warm-up (allocator, thread pool)
+            o.set_scales({n: 0.05 for n in synth.linear_names(cfg)})
+        return o, "W4A8 fake-quant op graph (oracle/w4a8_ref.py)"
+    return (sam_ref.EncoderOracle(cfg, st, precision=precision, linear_weights=lw, linear_bias=lb),
+            "fp32 CPU fake-quant op graph (oracle/sam_ref.py)")
+
+
+def _oracle_image(img0):
+    if img0 is not None:
+        return img0.detach().float().cpu().reshape(1, 3, 1024, 1024)
+    return torch.randn(1, 3, 1024, 1024, generator=torch.Generator().manual_seed(0))
+
+
+def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, groupsize: int = -1, runs: int = 3):
+    """Oracle restatement of the reference CPU fake-quant path on one 1024x1024 image, rank 0 only,
+    median of ``runs`` timed runs after one warm-up (every mode the same method).  With the bench
+    encoder (``enc``) and its image 0 (``img0``) the oracle is the encoder's own (``build_oracle``),
+    so its output doubles as the parity reference (returned second)."""
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
+    own = enc is not None and img0 is not None
+    o, what = build_oracle(model_name, mode, enc if own else None, groupsize)
+    img = _oracle_image(img0 if own else None)
+    o(img)   # warm-up (allocator, thread pool)
     times = []
     for _ in range(runs):
         t0 = time.perf_counter()
@@ -368,11 +387,36 @@ def cpu_baseline(model_name: str, mode: str = "w4a16", enc=None, img0=None, grou
         times.append(time.perf_counter() - t0)
     dt = statistics.median(times)
     src = "the bench encoder's own weights and image 0" if own else "seeded random weights"
-    how = f"median of {runs} runs after 1 warm-up" if runs > 1 else "one cold run (no warm-up)"
     return dict(value=round(1.0 / dt, 4), unit="img/s", cores=threads, kind="port",
-                sample=f"1 image, {model_name} {what} on {src}; {how} "
+                sample=f"1 image, {model_name} {what} on {src}; median of {runs} runs after 1 warm-up "
                        f"({', '.join(f'{r:.2f}' for r in times)} s), torch {threads} threads, CPU: {_cpu_model()}"
                 ), (ref if own else None)
+
+
+def parity_reference(model_name: str, mode: str, enc, img0, groupsize: int = -1):
+    """Parity-only oracle output (N > 1 runs: rank 0's image 0 is global image 0 at every N; no CPU
+    baseline is reported there)."""
+    torch.set_num_threads(_cpu_threads(parity_only=True))
+    o, _ = build_oracle(model_name, mode, enc, groupsize)
+    return o(_oracle_image(img0))
+
+
+def int8_reference_points(model_name: str, mode: str, enc, img0, groupsize: int = -1) -> dict:
+    """Reference points for the int8 modes' end-to-end parity (checker side): the SAME fake-quant
+    graph evaluated in float64 (``fp64``: how far the oracle's own rounding moves the chaotic int8
+    codes) and, for W4A8, the graph without its activation quantisers
+    (``int8_noise``: the W4A16 G1 output, tests/test_w4a8.py's noise reference)."""
+    torch.set_num_threads(_cpu_threads(parity_only=True))
+    img = _oracle_image(img0)
+    pts = {}
+    o64, _ = build_oracle(model_name, mode, enc, groupsize, precision="fp64")
+    pts["fp64"] = o64(img).float()
+    del o64
+    if mode == "w4a8":
+        o, _ = build_oracle(model_name, mode, enc, groupsize)
+        o.mode = "float"
+        pts["int8_noise"] = o(img)
+    return pts
 
 
 def mask_iou_report(emb: torch.Tensor, ref: torch.Tensor) -> dict:
@@ -416,31 +460,67 @@ def mask_iou_report(emb: torch.Tensor, ref: torch.Tensor) -> dict:
                                 "at 1024x1024 thresholded at 0; IoU = get_iou (script/evaluation2.py:156-167)")
 
 
-def parity_report(mode: str, mine: torch.Tensor, ref: torch.Tensor) -> dict:
+def _dist_stats(a: torch.Tensor, b: torch.Tensor) -> dict:
+    a, b = a.detach().double().cpu().flatten(), b.detach().double().cpu().flatten()
+    d = (a - b).abs()
+    return dict(max_abs=float(d.max()), mean_abs=float(d.mean()),
+                cosine=round(float((a * b).sum() / (a.norm() * b.norm())), 6))
+
+
+def parity_report(mode: str, mine: torch.Tensor, ref: torch.Tensor, points: dict | None = None) -> dict:
     """Encoder-output distance of the TIMED graph's own output (image 0 of the last timed replay,
-    fp32) from the oracle fed the same weights, scales and image, plus the mask IoU."""
+    fp32) from the oracle fed the same weights, scales and image, plus the mask IoU.
+
+    int8 modes: ``points`` (``int8_reference_points``) carry the oracle's own fp64-vs-fp32 distance
+    (max-abs, cosine, mask IoU) and, for W4A8, the int8 activation noise; ``pass`` is then gated
+    against them (W8A8: cosine >= 0.995 and mask IoU mean >= the fp64 self mean - 0.02; W4A8:
+    max-abs <= 1.5x the int8 noise, tests/test_w4a8.py:185, and the same mask IoU rule)."""
     mine = mine.detach().float()
-    d = (mine.cpu() - ref.float()).abs()
+    ref = ref.float()
+    st = _dist_stats(mine, ref)
     rec = {"image": 0, "source": "the timed HIP graph's own output buffer (image 0 of the last timed replay)",
-           "max_abs_vs_oracle": float(d.max()), "mean_abs": float(d.mean()), "ref_absmax": float(ref.abs().max())}
-    if mode == "w4a16":
-        rec.update(oracle="G1 (oracle/sam_ref.py: fp32 encoder, GPTQ weights s*(q-zp))", tolerance=1e-2,
-                   **{"pass": bool(float(d.max()) <= 1e-2)})
-    elif mode == "w4a8":
-        rec.update(oracle="W4A8 composition (oracle/w4a8_ref.py) with the engine's calibrated activation scales",
-                   tolerance=None, **{"pass": None},
-                   note="int8 activation quantisers make end-to-end codes chaotic; bound stated per stage "
-                        "(tests/test_w4a8.py stage-local parity) and statistically end to end (DESIGN.md sec. 5)")
-    else:
-        a, b = mine.cpu().double().flatten(), ref.double().flatten()
-        cos = float((a * b).sum() / (a.norm() * b.norm()))
-        rec.update(oracle="fq_vit W8A8 fake-quant graph (oracle/fq_ref.py) with the engine's weights and calibrated "
-                          "activation scales", cosine=round(cos, 6), tolerance="cosine >= 0.995 "
-                   "(tests/test_w8a8.py::test_w8a8_encoder_vs_golden)", **{"pass": bool(cos >= 0.995)})
+           "max_abs_vs_oracle": st["max_abs"], "mean_abs": st["mean_abs"], "ref_absmax": float(ref.abs().max())}
     try:
         rec.update(mask_iou_report(mine.reshape(1, 256, 64, 64), ref))
     except Exception as e:   # the report must not cost the throughput line
         rec["mask_iou_error"] = repr(e)[:200]
+    iou_ok = None
+    if points:
+        refp = {}
+        for k, v in points.items():
+            r = _dist_stats(v, ref)
+            try:
+                m = mask_iou_report(v.float().reshape(1, 256, 64, 64), ref)
+                r.update(mask_iou_min=m["mask_iou_min"], mask_iou_mean=m["mask_iou_mean"])
+            except Exception as e:  # noqa: BLE001
+                r["mask_iou_error"] = repr(e)[:200]
+            refp[k] = r
+        rec["reference_points"] = dict(refp, note="distance of each reference output from the fp32 oracle, "
+                                       "same image / weights / scales: fp64 = the oracle's own graph in float64 "
+                                       "(its self-distance), int8_noise = the graph without activation quantisers")
+        selfp = refp.get("fp64", {})
+        if "mask_iou_mean" in selfp and "mask_iou_mean" in rec:
+            iou_ok = bool(rec["mask_iou_mean"] >= selfp["mask_iou_mean"] - 0.02)
+    if mode == "w4a16":
+        rec.update(oracle="G1 (oracle/sam_ref.py: fp32 encoder, GPTQ weights s*(q-zp))", tolerance=1e-2,
+                   **{"pass": bool(st["max_abs"] <= 1e-2)})
+    elif mode == "w4a8":
+        rec.update(oracle="W4A8 composition (oracle/w4a8_ref.py) with the engine's calibrated activation scales")
+        noise = (points or {}).get("int8_noise")
+        if noise is not None:
+            nmax = rec["reference_points"]["int8_noise"]["max_abs"]
+            ok = st["max_abs"] <= 1.5 * nmax and iou_ok is not False
+            rec.update(tolerance=f"max-abs <= 1.5 x int8 noise ({1.5 * nmax:.4f}; tests/test_w4a8.py:185) and mask "
+                                 "IoU mean >= fp64 self mean - 0.02", **{"pass": bool(ok)})
+        else:
+            rec.update(tolerance="max-abs <= 0.35 (tests/test_w4a8.py:186)", **{"pass": bool(st["max_abs"] <= 0.35)})
+    else:
+        ok = st["cosine"] >= 0.995 and iou_ok is not False
+        rec.update(oracle="fq_vit W8A8 fake-quant graph (oracle/fq_ref.py) with the engine's weights and calibrated "
+                          "activation scales", cosine=st["cosine"],
+                   tolerance="cosine >= 0.995 (tests/test_w8a8.py::test_w8a8_encoder_vs_golden)"
+                             + (" and mask IoU mean >= fp64 self mean - 0.02" if iou_ok is not None else ""),
+                   **{"pass": bool(ok)})
     return rec
 
 
@@ -515,12 +595,14 @@ def dry_run(args, rank: int, world: int) -> None:
     start, stop = sdist.shard(gb, rank, world)
     imgs = local_images(start, stop, torch.device("cpu"), torch.float32, size=32)
     enc = random_quant_encoder("vit_b", -1, device="cpu", depth=1, img_size=64, init=(rank == 0))
+    t_init = sdist.warm_up_collective()
     t0 = time.perf_counter()
     nbytes = sdist.broadcast_state(enc, src=0)
     t_bc = time.perf_counter() - t0
     wsum = float(sum(t.double().sum() for t in enc.state_dict().values() if torch.is_tensor(t)))
     rec = dict(rank=rank, shard=[start, stop], image_checksums=[float(x.double().sum()) for x in imgs],
-               state_checksum=wsum, broadcast_bytes=nbytes, broadcast_s=round(t_bc, 4))
+               state_checksum=wsum, broadcast_bytes=nbytes, broadcast_s=round(t_bc, 4),
+               first_collective_s=round(t_init, 4))
     on = dist.is_initialized()
     recs = [None] * world
     if on:
@@ -546,11 +628,14 @@ def build_mode(mode: str, model: str, groupsize: int, rank: int, dev):
     from samq.synthetic import random_fq_encoder, random_quant_encoder
     t_bc = 0.0
     if mode == "w8a8":
-        return random_fq_encoder(model, device=dev), 0, 0.0
+        return random_fq_encoder(model, device=dev), 0, 0.0, 0.0
     # model.half() as the reference's entry point runs it (gptq4sam_infer.py:59-79): the fp16
     # parameter values are what the engine and the parity oracle both see
     enc = random_quant_encoder(model, groupsize, device=dev, init=(rank == 0)).half()
     torch.cuda.synchronize()
+    # the first collective creates the communicator (RCCL set-up) and waits for the slowest rank's
+    # model build: timed on its own, so the broadcast time below is the transfer alone
+    t_init = sdist.warm_up_collective(dev)
     tb = time.perf_counter()
     nbytes = sdist.broadcast_state(enc, src=0)
     torch.cuda.synchronize()
@@ -560,7 +645,7 @@ def build_mode(mode: str, model: str, groupsize: int, rank: int, dev):
         gcal = torch.Generator(device="cpu").manual_seed(99)
         cal = torch.randn((1, 3, 1024, 1024), generator=gcal).to(dev, torch.float16)
         samq.calibrate_act_quant(enc, enc.module_forward, [cal])
-    return enc, nbytes, t_bc
+    return enc, nbytes, t_bc, t_init
 
 
 def run_mode(mode: str, args, rank: int, world: int, dev, batch: int, lanes: int, *, headline: bool):
@@ -572,14 +657,14 @@ def run_mode(mode: str, args, rank: int, world: int, dev, batch: int, lanes: int
     model = (args.model if headline else "") or ("vit_b" if mode == "w8a8" else "vit_h")
     groupsize = args.groupsize if (headline and mode == "w4a16") else -1
     t0 = time.time()
-    enc, nbytes, t_bc = build_mode(mode, model, groupsize, rank, dev)
+    enc, nbytes, t_bc, t_init = build_mode(mode, model, groupsize, rank, dev)
     eng = enc.engine()
     if headline and args.fold_ln:
         eng.fold_ln = True
     if headline and args.lane_stagger is not None:
         eng.lane_stagger = args.lane_stagger
     log(f"[rank {rank}] {mode} model ready in {time.time() - t0:.1f}s (broadcast {nbytes / 1e6:.1f} MB "
-        f"in {t_bc * 1e3:.1f} ms)")
+        f"in {t_bc * 1e3:.1f} ms after a {t_init * 1e3:.1f} ms first collective)")
 
     gb = world * batch
     start, stop = sdist.shard(gb, rank, world)
@@ -620,9 +705,11 @@ def run_mode(mode: str, args, rank: int, world: int, dev, batch: int, lanes: int
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     if on:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed, t_bc, t_init], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        elapsed, t_bc_max, t_init_max = t.tolist()
+    else:
+        t_bc_max, t_init_max = t_bc, t_init
     out0 = holder["out"][0:1].float().clone() if stop > start else None
 
     rows = stop - start
@@ -684,14 +771,24 @@ def run_mode(mode: str, args, rank: int, world: int, dev, batch: int, lanes: int
                 "frac_of_fp16_peak": round(e2e_tflops / PEAK_FP16_TFLOPS, 4),
                 "frac_of_int8_peak": round(e2e_tflops / (2 * PEAK_FP16_TFLOPS), 4)},
         "dist": {"backend": dist.get_backend() if on else None, "world_size_seen": world,
-                 "broadcast_bytes": nbytes, "broadcast_ms": round(t_bc * 1e3, 2), "rank0_shard": [start, stop]},
+                 "broadcast_bytes": nbytes, "broadcast_ms": round(t_bc_max * 1e3, 2),
+                 "broadcast_GBps": round(nbytes / t_bc_max / 1e9, 2) if nbytes and t_bc_max > 0 else None,
+                 "first_collective_ms": round(t_init_max * 1e3, 2),
+                 "broadcast_method": "max over ranks; timed after a one-element all_reduce that creates the "
+                                     "communicator and waits for rank 0's model build (first_collective_ms)",
+                 "rank0_shard": [start, stop]},
         "parity": None, "cpu_baseline": None,
     }
-    if world == 1 and not args.no_cpu_baseline and out0 is not None:
-        # checker leg, after the timed region: the oracle fed this encoder's weights and image 0
-        rec["cpu_baseline"], ref = cpu_baseline(model, mode, enc, img[0], groupsize, runs=3 if headline else 1)
-        if ref is not None:
-            rec["parity"] = parity_report(mode, out0, ref)
+    if not args.no_cpu_baseline and out0 is not None:
+        # checker leg, after the timed region: the oracle fed this encoder's weights and rank 0's
+        # image 0 (= global image 0 at every N); the CPU baseline is timed at N = 1 only, and the
+        # other ranks wait at the final barrier meanwhile
+        if world == 1:
+            rec["cpu_baseline"], ref = cpu_baseline(model, mode, enc, img[0], groupsize)
+        else:
+            ref = parity_reference(model, mode, enc, img[0], groupsize)
+        points = int8_reference_points(model, mode, enc, img[0], groupsize) if mode != "w4a16" else None
+        rec["parity"] = parity_report(mode, out0, ref, points)
     del eng, enc, img, holder
     return rec
 
@@ -734,9 +831,13 @@ def main():
     if args.dry_run:
         return dry_run(args, rank, world)
 
-    # one GPU per local rank; more ranks than GPUs (a gloo rehearsal of the N-rank path on a smaller
-    # box) share them round-robin
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    # one GPU per local rank; more ranks than GPUs only for a gloo rehearsal of the N-rank path on a
+    # smaller box (ranks then share the GPUs round-robin) -- never silently under RCCL
+    lr, ndev = int(os.environ.get("LOCAL_RANK", "0")), torch.cuda.device_count()
+    if lr >= ndev and (dist.is_initialized() and dist.get_backend() != "gloo" or ndev == 0):
+        raise SystemExit(f"LOCAL_RANK {lr} but only {ndev} visible GPUs: one rank per GPU (a shared-GPU "
+                         "rehearsal needs --backend gloo)")
+    dev = torch.device("cuda", lr % ndev)
     torch.cuda.set_device(dev)
     mode = args.mode
     batch = args.batch or default_batch(mode, world)

@@ -122,7 +122,7 @@ class EncoderOracle:
     def __init__(self, cfg: dict, state: dict, precision: str = "fp32",
                  linear_weights: dict | None = None, linear_bias: dict | None = None):
         self.cfg = cfg
-        self.dtype = {"fp32": torch.float32, "fp16": torch.float16}[precision]
+        self.dtype = {"fp32": torch.float32, "fp16": torch.float16, "fp64": torch.float64}[precision]
         self.p = {k: _t(v, self.dtype) for k, v in state.items()}
         for name, wt in (linear_weights or {}).items():
             self.p[name + ".weight"] = _t(wt, self.dtype)

@@ -184,7 +184,8 @@ __device__ __forceinline__ float2_t q8_recip2(float2_t v, float inv) {
 }
 // four codes (integer floats) -> their int8 bytes in one dword: v_cvt_pk_u8_f32 of code + 128 per
 // byte, then the sign bit flipped back per byte.  The conversion saturates to [0, 255] (and rounds to
-// nearest even; gfx950, tools/probe_cvt_u8.hip), so codes outside [-128, 127] come out clamped
+// nearest even; gfx950, tools/probe_cvt_u8.hip -> profiles/r6_probe_cvt_u8.log), so codes outside
+// [-128, 127] come out clamped
 __device__ __forceinline__ uint32_t q8_pack4(float c0, float c1, float c2, float c3) {
   uint32_t w = __builtin_amdgcn_cvt_pk_u8_f32(c0 + 128.f, 0, 0u);
   w = __builtin_amdgcn_cvt_pk_u8_f32(c1 + 128.f, 1, w);

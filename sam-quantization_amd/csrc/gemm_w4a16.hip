@@ -2000,11 +2000,13 @@ static int launch_epi(const GemmArgs& a, int cfg, hipStream_t st) {
   if (cfg >= 50 && cfg < 200) {   // ping-pong kernels
     if (GR) {   // grouped weights: the per-group scale / zero row rides in the ring (VAR & 512)
       switch (cfg) {
-        // the group's scale / zero words prefetched into VGPRs (VAR & (1 << 23)): 4 slots, lookahead 3
-        case 57: case 112: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 4096 | (1 << 23)>(a, st);
-        // the group row in the ring: 3 slots, lookahead 2 (four 40 KiB stages fill the 160 KiB LDS,
-        // the group row needs 640 B more)
-        case 114: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
+        // the group's scale / zero words prefetched into VGPRs (VAR & (1 << 23)): 4 slots, lookahead 3.
+        // Selectable, not the default: measured neutral (155.6 vs 155.3 img/s), and its inline-asm
+        // loads leave the compiler free to move the not-yet-filled registers before their counted wait
+        case 112: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 4096 | (1 << 23)>(a, st);
+        // the group row in the ring (the grouped cfg 57): 3 slots, lookahead 2 (four 40 KiB stages
+        // fill the 160 KiB LDS, the group row needs 640 B more)
+        case 57: case 114: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512>(a, st);
         case 64: return launch_pp2<2, 4, 2, 2, 3, 2, EPI, 512 | 16>(a, st);   // (slower than 57 on every shape)
         // register rows (VAR & (1 << 23)): no group row in the ring -> 4 slots / lookahead 3
         case 113: return launch_pp2<2, 4, 2, 2, 4, 3, EPI, 512 | 16 | 4096 | (1 << 23)>(a, st);

@@ -73,3 +73,19 @@ def gather_embeddings(local: torch.Tensor, dst: int = 0):
     parts = [torch.empty_like(local) for _ in range(dist.get_world_size())] if dist.get_rank() == dst else None
     dist.gather(local, parts, dst=dst)
     return torch.cat(parts) if parts is not None else None
+
+
+def warm_up_collective(device=None) -> float:
+    """One-element ``all_reduce`` before the weight broadcast: the first collective of a process
+    group creates the communicator (RCCL's set-up) and waits for the slowest rank, so timing the
+    broadcast after it measures the transfer alone.  Returns its seconds (0 without a group)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0.0
+    import time
+    on_gpu = device is not None and torch.device(device).type == "cuda"
+    t0 = time.perf_counter()
+    t = torch.zeros(1, device=device)
+    dist.all_reduce(t)
+    if on_gpu:
+        torch.cuda.synchronize(device)
+    return time.perf_counter() - t0

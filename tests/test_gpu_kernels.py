@@ -170,12 +170,15 @@ def test_w4a16_gemm_pingpong_grouped(cuda, cfg, groupsize, epi):
 @pytest.mark.parametrize("groupsize", [64, 128, 192, 256])
 def test_w4a16_grouped_register_rows(cuda, cfg, base, groupsize):
     """Grouped ping-pong with register rows (the group's scale / zero words loaded into VGPRs ahead
-    of the group, counted in the ring's vmcnt; 4 ring slots; cfg 112 = the grouped cfg 57) against
-    the ring-row form (cfg 114, the group row as one more LDS-DMA piece per stage): identical
-    bits (same unpack, same MFMA order) for 1 .. 80 K tiles, 1 .. 4 K tiles per group, every
-    epilogue, plus the oracle at the largest K."""
+    of the group, counted in the ring's vmcnt; 4 ring slots; cfg 112, selectable) against the
+    ring-row form (cfg 114 = the grouped cfg 57, the group row as one more LDS-DMA piece per
+    stage): identical bits (same unpack, same MFMA order) for 1 .. 80 K tiles, 1 .. 4 K tiles per
+    group, every epilogue, plus the oracle at the largest K.  Groupsize 192 (3 K tiles per group)
+    runs multi-group shapes too: K = 576 / 960 / 1152 (3, 5, 6 groups; at K = 960 the ring's last
+    stages fall inside the last group)."""
     from samq import ops
-    shapes = [(300, 64 * t, 256) for t in (1, 2, 3, 4, 5, 7)] + [(333, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280)]
+    shapes = [(300, 64 * t, 256) for t in (1, 2, 3, 4, 5, 7)] + [(300, 576, 256), (300, 960, 256), (260, 1152, 256)] \
+        + [(333, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280)]
     for m, k, n in shapes:
         if k % groupsize:
             continue

@@ -253,3 +253,27 @@ def test_bench_parity_report_cpu():
     assert rec["mask_iou_min"] == 1.0 and rec["masks"] == 20
     bad = bench.parity_report("w8a8", -ref, ref)
     assert bad["pass"] is False and bad["cosine"] < -0.99 and bad["mask_iou_min"] < 0.9
+
+
+def test_bench_int8_parity_gate_cpu():
+    """The int8 modes' parity stanza is gated against its reference points:
+    the oracle's own fp64-vs-fp32 distance (mask IoU) and, for W4A8, the int8 activation noise
+    (max-abs <= 1.5x, tests/test_w4a8.py:185); ``pass`` is a boolean, never null."""
+    import bench
+    g = torch.Generator().manual_seed(1)
+    ref = torch.randn((1, 256, 64, 64), generator=g) * 0.5
+    near = ref + 0.01 * torch.randn(ref.shape, generator=g)
+    noise = ref + 0.05 * torch.randn(ref.shape, generator=g)
+    pts = {"fp64": near, "int8_noise": noise}
+    ok = bench.parity_report("w4a8", near.clone(), ref, pts)
+    assert ok["pass"] is True and "fp64" in ok["reference_points"]
+    assert ok["reference_points"]["fp64"]["mask_iou_mean"] > 0.9
+    far = ref + 0.5 * torch.randn(ref.shape, generator=g)
+    assert bench.parity_report("w4a8", far, ref, pts)["pass"] is False      # > 1.5x the noise
+    assert bench.parity_report("w8a8", near.clone(), ref, {"fp64": near})["pass"] is True
+    # half the channels sign-flipped: fails (cosine and masks)
+    flip = ref.clone()
+    flip[:, :128] = -flip[:, :128]
+    rec = bench.parity_report("w8a8", flip, ref, {"fp64": ref.clone()})
+    assert rec["pass"] is False
+    assert bench.parity_report("w4a8", near.clone(), ref)["pass"] is True   # no points: absolute 0.35

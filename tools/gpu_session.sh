@@ -11,6 +11,8 @@
 #   bench | bench48 | bench88 | benchg       full bench lines (w4a16 / w4a8 / w8a8 / G=128)
 #   benchq | b48q | b88q   bench lines without CPU baseline
 #   instep | instep48 | instep88 | instepg   rocprofv3 in-step kernel traces (tools/instep_profile.sh)
+#   instep8                the same for config 4's per-GPU geometry (B = 8, 4 lanes: the N > 1 line's roofline)
+#   rehearse               the N = 2 bench line on this one GPU (gloo, both ranks on cuda:0)
 #   pmc                    PMC HBM traffic of every mode (tools/pmc_all.sh)
 #   publish=<round>        copy this build's in-step traces and the PMC summaries (wrapped with their
 #                          source line as profiles/<round>_pmc_traffic_<mode>_m<rows>.json) into
@@ -75,6 +77,8 @@ for step in "$@"; do
     instep48) run instep48 500 bash tools/instep_profile.sh w4a8 ;;
     instep88) run instep88 500 bash tools/instep_profile.sh w8a8 ;;
     instepg)  run instepg 500 bash tools/instep_profile.sh w4a16 --groupsize 128 ;;
+    instep8)  run instep8 500 bash tools/instep_profile.sh w4a16 --batch 8 ;;
+    rehearse) run rehearse 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 2 ;;
     pmc)      run pmc 900 bash tools/pmc_all.sh ;;
     publish=*) H=$(python3 -c "import bench; print(bench.source_hash())")
               cp gpurun_out/instep_*_"$H".json gpurun_out/instep_*_"$H"_wholerun_stats.csv profiles/ || exit 1
