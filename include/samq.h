@@ -157,6 +157,18 @@ int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* wpacked, con
                        int K, int groupsize, int epilogue, float a_scale, float out_scale, int cfg,
                        hipStream_t stream);
 
+/* Per-channel W4A8 GEMM with the zero point's row sums moved to the producers (round 6):
+ * rowsum_in (optional, int32 [M]) = S[m] = sum_k A[m, k] of the int8 input rows -- the zero-point
+ * ping-pong (cfg 86 / 93) then subtracts zp[n] * S[m] without re-summing A per column tile; kernels
+ * without the row-sum form ignore it.  rowsum_out (optional, int32 [M], ZEROED by the caller;
+ * epilogue Q8 / Q8_GELU only) accumulates the row sums of the int8 output codes with atomics, the
+ * next GEMM's rowsum_in (replaces the per-tile row sums of quant_linear.py:299-343's zero-point
+ * subtraction; fq_vit uniform.py:23-45 codes).  Outputs are bit-identical to samq_w4a8_gemm_cfg. */
+int samq_w4a8_gemm_rs(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                      const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N, int K,
+                      int epilogue, float a_scale, float out_scale, const int32_t* rowsum_in,
+                      int32_t* rowsum_out, int cfg, hipStream_t stream);
+
 /* Both int8 GEMMs with an explicit weight format (0 = W8 packed, 1 = W4 layout 3) and tile
  * config (0 = automatic; 81 256x256, 82 128x256, 83 128x128, 84 64x64); for tuning and tests. */
 int samq_i8_gemm_cfg(const int8_t* A, int64_t lda, int bfmt, const void* wpacked, const float* wscale,
@@ -246,6 +258,12 @@ int samq_layernorm_mean(const void* x, void* y, const float* gamma, const float*
 int samq_layernorm_q(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
                      int C, float eps, int flags, float in_scale, float out_scale,
                      hipStream_t stream);
+/* samq_layernorm_q with int8-code output (SAMQ_LN_OUT_I8) plus rowsum[r] = sum_c y[r, c] (int32
+ * [rows], the W4A8 GEMM's rowsum_in) and, when zero_rows is not null, zero_rows[r] = 0 (the
+ * accumulator of the next int8-code GEMM's rowsum_out). */
+int samq_layernorm_q_rs(const void* x, void* y, const float* gamma, const float* beta, int64_t rows,
+                        int C, float eps, int flags, float in_scale, float out_scale, int32_t* rowsum,
+                        int32_t* zero_rows, hipStream_t stream);
 
 /* Residual add + LayerNorm (Block.forward's x = x + attn(...) / x = x + mlp(...) followed by the
  * next norm, image_encoder.py:199-207): x f32 [rows, C] += delta (f16 with SAMQ_LN_DELTA_F16,

@@ -33,6 +33,12 @@ struct I8Epi {
   int64_t ldr;
   int rmod;               // > 0: residual row = output row % rmod (pos_embed codes shared by images)
   int kpg;                // grouped W4 (GRP kernels): K tiles (128) per weight group
+  // W4A8 row sums (round 6): rs_in = S[m] = sum_k A[m, k] of the int8 input rows, emitted by the
+  // producer of A (LN-q, the lin1 epilogue) so the zero-point ping-pong (cfg 86 / 93) does not
+  // recompute it per column tile; rs_out (int8-code epilogues): S of the OUTPUT rows accumulated
+  // with one int32 atomic per row and 16 x (WN / 16) codes -- the caller zeroes it first
+  const int* rs_in;
+  int* rs_out;
 };
 
 // Implicit-GEMM A operand (AG != 0): the int8 codes are gathered from an image / feature map
@@ -180,9 +186,11 @@ __device__ __forceinline__ void i8_epilogue_slice(int i, const AccV (&acc)[TM][T
       }
     } else {   // int8 codes, 16 columns per lane-store
       constexpr int C16 = WN / 16;
+      static_assert(C16 >= 1 && 64 % C16 == 0, "int8 store: a row's lanes are C16 consecutive lanes");
 #pragma unroll
       for (int j = 0; j < (32 * C16 + 63) / 64; ++j) {
         const int idx = j * 64 + lane;
+        int rsum = 0;   // this lane's 16 codes summed (rs_out)
         if (idx < 32 * C16) {
           const int rl = idx / C16, c16 = idx % C16;
           const int row = row_base + i * 32 + rl;
@@ -219,7 +227,17 @@ __device__ __forceinline__ void i8_epilogue_slice(int i, const AccV (&acc)[TM][T
               o[w] = q8_pack4(cq[0], cq[1], cq[2], cq[3]);
             }
             *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
+            if (ep_args.rs_out) {
+#pragma unroll
+              for (int w = 0; w < 4; ++w) rsum = __builtin_amdgcn_sdot4((int)o[w], 0x01010101, rsum, false);
+            }
           }
+        }
+        if (ep_args.rs_out) {   // the row's C16 lanes reduce, one int32 atomic per row of the slice
+#pragma unroll
+          for (int off = 1; off < C16; off <<= 1) rsum += __shfl_xor(rsum, off, 64);
+          const int rl = idx / C16, row = row_base + i * 32 + rl;
+          if (idx < 32 * C16 && idx % C16 == 0 && row < M) atomicAdd(ep_args.rs_out + row, rsum);
         }
       }
     }
@@ -607,10 +625,18 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   uint32_t kLo = 0x0F0F0F0Fu;
   asm volatile("" : "+v"(kLo));
   constexpr bool ZPS = (VAR & 8) != 0;
+  // VAR & 64 (with ZPS): the row sums come from the producer of A (ep_args.rs_in), loaded once here
+  // -- older than every LDS-DMA piece, so the ring's counted waits retire it on the way -- instead
+  // of 8 v_dot4 + 2 LDS reads per wave and phase
+  constexpr bool RSIN = ZPS && (VAR & 64) != 0;
   static_assert(!ZPS || TM == WAVES_N, "row sums: wave wn sums M block wn");
   const int rs_row = wm * WM + wn * 32 + (lane & 31);
   const int rs_off = rs_row * ROWB, rs_swz = (rs_row >> 1) & 7;
   int rsum = 0;
+  if constexpr (RSIN) {
+    const int r = m0 + rs_row;
+    rsum = ep_args.rs_in[r < M ? r : M - 1];
+  }
 
   // ---- prologue: K tiles 0 .. LA-1 in flight, tile 0 retired + visible; group 1 lags a barrier
   const int pro = kt_count < LA ? kt_count : LA;
@@ -653,7 +679,7 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
 #pragma unroll
         for (int s = 0; s < 2; ++s)
           af[i][s] = *(const int4_t*)(st + a_off[i] + (((2 * (2 * p + s) + hsel) ^ a_swz[i]) << 4));
-      if constexpr (ZPS) {
+      if constexpr (ZPS && !RSIN) {
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int4_t x = *(const int4_t*)(st + rs_off + (((2 * (2 * p + s) + hsel) ^ rs_swz) << 4));
@@ -730,7 +756,7 @@ void i8_gemm_pp2(const int8_t* __restrict__ A, int64_t lda, const char* __restri
   __syncthreads();
   if constexpr (ZPS) {
     int* s_lds = (int*)(smem + NW * EP_BYTES);
-    rsum += __shfl_xor(rsum, 32, 64);   // the two k halves of the row
+    if constexpr (!RSIN) rsum += __shfl_xor(rsum, 32, 64);   // the two k halves of the row
     if (lane < 32) s_lds[rs_row] = rsum;
     __syncthreads();
     int zpv[TN];
@@ -1038,10 +1064,12 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
       if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 85 is the W4 ping-pong kernel");
     case 86:
-      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8>(a, st);
+      if constexpr (BF == BF_W4)
+        return a.ep.rs_in ? launch_i8_pp2<EPI, 3, 2, 8 | 64>(a, st) : launch_i8_pp2<EPI, 3, 2, 8>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 86 is the W4 ping-pong kernel");
     case 93:   // cfg 86 with the LDS-DMA pieces spread through the MFMA bursts
-      if constexpr (BF == BF_W4) return launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
+      if constexpr (BF == BF_W4)
+        return a.ep.rs_in ? launch_i8_pp2<EPI, 3, 2, 8 | 16 | 64>(a, st) : launch_i8_pp2<EPI, 3, 2, 8 | 16>(a, st);
       else return fail(SAMQ_ERR_INVALID, "i8_gemm: cfg 93 is the W4 ping-pong kernel");
 #ifdef SAMQ_TUNING
     case 99:   // tile ping-pong: one group's epilogue under the other group's main loop (correct, slower)
@@ -1267,6 +1295,33 @@ extern "C" int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* w
   I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
            I8Epi{a_scale, 0.f, 0.f, out_scale, nullptr, 0, 0, groupsize / 128}, I8Gather{0, 0, 0}};
   return i8_dispatch_grouped(a, epilogue, cfg, stream);
+}
+
+extern "C" int samq_w4a8_gemm_rs(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,
+                                 const int32_t* qzeros, const float* bias, void* C, int64_t ldc, int M, int N, int K,
+                                 int epilogue, float a_scale, float out_scale, const int32_t* rowsum_in,
+                                 int32_t* rowsum_out, int cfg, hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
+  SAMQ_REQUIRE(epilogue != SAMQ_EPI_Q8_RES, SAMQ_ERR_INVALID, "w4a8_gemm_rs: Q8_RES is a W8A8 epilogue");
+  SAMQ_REQUIRE(!rowsum_out || epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_GELU, SAMQ_ERR_INVALID,
+               "w4a8_gemm_rs: rowsum_out needs an int8-code epilogue (Q8 / Q8_GELU)");
+  SAMQ_REQUIRE(M < (1 << 30) && (!rowsum_in || K < 65536), SAMQ_ERR_UNSUPPORTED,
+               "w4a8_gemm_rs: row sums need K < 65536");
+  SAMQ_REQUIRE(A && wpacked && wscale && qzeros && C, SAMQ_ERR_INVALID, "w4a8_gemm_rs: null pointer");
+  SAMQ_REQUIRE(lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm_rs: A must be 16-byte aligned with lda >= K, lda % 16 == 0");
+  SAMQ_REQUIRE(M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 64 == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm_rs: K % 128 == 0 and N % 64 == 0 required");
+  const bool q8 = epilogue == SAMQ_EPI_Q8 || epilogue == SAMQ_EPI_Q8_GELU;
+  const bool f32 = epilogue == SAMQ_EPI_RESADD_F32 || epilogue == SAMQ_EPI_F32;
+  SAMQ_REQUIRE(ldc >= N && ((uintptr_t)C & 15) == 0 && ldc % (q8 ? 16 : (f32 ? 4 : 8)) == 0, SAMQ_ERR_INVALID,
+               "w4a8_gemm_rs: C must be 16-byte aligned rows, ldc >= N");
+  SAMQ_REQUIRE(!q8 || out_scale > 0.f, SAMQ_ERR_INVALID, "w4a8_gemm_rs: quantising epilogue needs out_scale > 0");
+  if (cfg <= 0) cfg = i8_pick_cfg(M, N, BF_W4);
+  SAMQ_REQUIRE(i8_cfg_bn(cfg) > 0 && N % i8_cfg_bn(cfg) == 0, SAMQ_ERR_INVALID, "w4a8_gemm_rs: N not divisible by tile");
+  I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
+           I8Epi{a_scale, 0.f, 0.f, out_scale, nullptr, 0, 0, 0, rowsum_in, rowsum_out}, I8Gather{0, 0, 0}};
+  return i8_dispatch(a, BF_W4, epilogue, cfg, stream);
 }
 
 extern "C" int samq_w4a8_gemm(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
                                                         float eps, float in_scale, float out_scale,
                                                         float* __restrict__ mean_out,
                                                         const void* __restrict__ delta = nullptr,
-                                                        float* xres = nullptr) {
+                                                        float* xres = nullptr, int* __restrict__ rs_out = nullptr,
+                                                        int* __restrict__ rs_zero = nullptr) {
   static_assert(ADD == 0 || IN == LN_F32, "residual add: f32 rows");
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
@@ -111,6 +112,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
       }
     }
     const float rstd = rsqrtf(wave_sum_valu(q) / (float)C + eps);
+    int rsi = 0;   // LN_I8 with rs_out: the row's codes summed (the W4A8 GEMM's zero-point row sum)
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int j = lane + 64 * i;
@@ -130,12 +132,19 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const void* __restrict__
           const float inv = 1.0f / out_scale, lim = 130.0f * out_scale;   // (loop-invariant: hoisted)
           const float2_t c01 = q8_exact2(float2_t{o[0], o[1]}, out_scale, inv, lim);
           const float2_t c23 = q8_exact2(float2_t{o[2], o[3]}, out_scale, inv, lim);
-          ((uint32_t*)y)[row * nvec + j] = q8_pack4(c01.x, c01.y, c23.x, c23.y);
+          const uint32_t wq = q8_pack4(c01.x, c01.y, c23.x, c23.y);
+          ((uint32_t*)y)[row * nvec + j] = wq;
+          if (rs_out) rsi = __builtin_amdgcn_sdot4((int)wq, 0x01010101, rsi, false);
         } else {
           ((half4_t*)y)[row * nvec + j] = half4_t{(_Float16)o[0], (_Float16)o[1], (_Float16)o[2], (_Float16)o[3]};
         }
       }
     }
+    if (OUT == LN_I8 && rs_out) {   // |sum| <= 128 C < 2^24: the f32 wave sum is exact
+      const float t = wave_sum_valu((float)rsi);
+      if (lane == 0) rs_out[row] = (int)t;
+    }
+    if (rs_zero && lane == 0) rs_zero[row] = 0;   // the next GEMM's rs_out accumulator
   }
 }
 
@@ -152,7 +161,7 @@ static int ln_rpw(int flags) {
 
 static int ln_launch(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C, float eps,
                      int in, int out, float in_scale, float out_scale, int rpw, hipStream_t stream,
-                     float* mean_out = nullptr) {
+                     float* mean_out = nullptr, int* rs_out = nullptr, int* rs_zero = nullptr) {
   if (rows == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(x && y && gamma && beta, SAMQ_ERR_INVALID, "layernorm: null pointer");
   SAMQ_REQUIRE(C > 0 && C % 4 == 0 && C <= 4096, SAMQ_ERR_INVALID, "layernorm: C must be a multiple of 4, <= 4096");
@@ -163,9 +172,9 @@ static int ln_launch(const void* x, void* y, const float* gamma, const float* be
   const dim3 grid((unsigned)((rows + 4 * rpw - 1) / (4 * rpw)));
 #define LN_R(I, O, V) \
   do { \
-    if (rpw == 1) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
-    else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 2>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
-    else hipLaunchKernelGGL((layernorm_kernel<I, O, V, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out); \
+    if (rpw == 1) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 1>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out, nullptr, nullptr, rs_out, rs_zero); \
+    else if (rpw == 2) hipLaunchKernelGGL((layernorm_kernel<I, O, V, 2>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out, nullptr, nullptr, rs_out, rs_zero); \
+    else hipLaunchKernelGGL((layernorm_kernel<I, O, V, 4>), grid, dim3(256), 0, stream, x, y, gamma, beta, rows, C, eps, in_scale, out_scale, mean_out, nullptr, nullptr, rs_out, rs_zero); \
   } while (0)
 #define LN_V(I, O) \
   do { \
@@ -238,4 +247,20 @@ extern "C" int samq_layernorm_q(const void* x, void* y, const float* gamma, cons
   const int out = (flags & SAMQ_LN_OUT_I8) ? ((flags & SAMQ_LN_OUT_F32) ? LN_FQ32 : LN_I8)
                                            : ((flags & SAMQ_LN_OUT_F32) ? LN_F32 : LN_F16);
   return ln_launch(x, y, gamma, beta, rows, C, eps, in, out, in_scale, out_scale, ln_rpw(flags), stream);
+}
+
+// LN-q with the output rows' code sums (round 6): rowsum[r] = sum_c y[r, c] (int8 codes, SAMQ_LN_OUT_I8
+// required) for the W4A8 zero-point GEMM that reads y; zero_rows (optional) [rows] int32 set to 0 --
+// the accumulator the next int8-code GEMM epilogue adds its output row sums into
+extern "C" int samq_layernorm_q_rs(const void* x, void* y, const float* gamma, const float* beta, int64_t rows, int C,
+                                   float eps, int flags, float in_scale, float out_scale, int32_t* rowsum,
+                                   int32_t* zero_rows, hipStream_t stream) {
+  SAMQ_REQUIRE((flags & SAMQ_LN_OUT_I8) && !(flags & SAMQ_LN_OUT_F32), SAMQ_ERR_INVALID,
+               "layernorm_q_rs: row sums of int8-code outputs only (SAMQ_LN_OUT_I8)");
+  SAMQ_REQUIRE(rows == 0 || rowsum, SAMQ_ERR_INVALID, "layernorm_q_rs: null rowsum");
+  SAMQ_REQUIRE(!(flags & SAMQ_LN_IN_I8) || in_scale > 0.f, SAMQ_ERR_INVALID, "layernorm_q_rs: in_scale must be > 0");
+  SAMQ_REQUIRE(out_scale > 0.f, SAMQ_ERR_INVALID, "layernorm_q_rs: out_scale must be > 0");
+  const int in = (flags & SAMQ_LN_IN_I8) ? LN_I8 : ((flags & SAMQ_LN_IN_F16) ? LN_F16 : LN_F32);
+  return ln_launch(x, y, gamma, beta, rows, C, eps, in, LN_I8, in_scale, out_scale, ln_rpw(flags), stream, nullptr,
+                   rowsum, zero_rows);
 }

@@ -70,6 +70,8 @@ SIGNATURES = {
                               _f32, _f32, _vp]),
     "samq_w4a8_gemm_cfg": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _i32,
                                   _f32, _f32, _i32, _vp]),
+    "samq_w4a8_gemm_rs": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _i32, _f32, _f32,
+                                 _vp, _vp, _i32, _vp]),
     "samq_i8_gemm_cfg": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32,
                                 _i32, _f32, _f32, _f32, _f32, _i32, _vp]),
     "samq_w8a8_conv_gemm": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32,
@@ -83,6 +85,7 @@ SIGNATURES = {
     "samq_layernorm": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp]),
     "samq_layernorm_mean": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _vp, _vp]),
     "samq_layernorm_q": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp]),
+    "samq_layernorm_q_rs": (_i32, [_vp, _vp, _vp, _vp, _i64, _i32, _f32, _i32, _f32, _f32, _vp, _vp, _vp]),
     "samq_rel_attention": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _vp]),
     "samq_rel_attention_q": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _f32, _vp]),
     "samq_attention_relbias": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _f32, _vp]),

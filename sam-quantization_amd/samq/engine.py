@@ -59,6 +59,11 @@ class EncoderEngine:
         # (x += y in f32); "ln32" = the GEMM stores y (f32) and the next LayerNorm adds it
         # (samq_add_layernorm, bit-identical x); "ln16" = the same with y stored as f16
         self.res_mode = "epi"
+        # W4A8 (per-channel weights, res_mode "epi"): the zero-point row sums S[m] of each int8 GEMM
+        # input come from its producer -- LN-q for qkv / lin1, lin1's Q8_GELU epilogue (int32 atomics)
+        # for lin2 -- instead of every column tile of the ping-pong GEMM re-summing its A rows;
+        # bit-identical either way (an in-graph A/B knob)
+        self.rowsums = True
         # timing-only A/B knob (tools): launches to leave out of the W4A16 block ("ln", "win",
         # "glob") -- the output is wrong; the empty default runs everything
         self.skip = frozenset()
@@ -169,7 +174,9 @@ class EncoderEngine:
             if self.w4a8:
                 bufs.update(xn8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
                             att8=torch.empty((b, g, g, c), dtype=torch.int8, device=dev),
-                            hid8=torch.empty((b, g, g, hid), dtype=torch.int8, device=dev))
+                            hid8=torch.empty((b, g, g, hid), dtype=torch.int8, device=dev),
+                            rs_x=torch.empty((b * g * g,), dtype=torch.int32, device=dev),
+                            rs_h=torch.empty((b * g * g,), dtype=torch.int32, device=dev))
                 del bufs["xn"], bufs["hid"], bufs["att"]
             self._bufs[(b, lane)] = bufs
         return bufs
@@ -208,13 +215,17 @@ class EncoderEngine:
         mark = mark or (lambda k: None)
         x, xn8, qkv, att8, hid8 = bufs["x"], bufs["xn8"], bufs["qkv"], bufs["att8"], bufs["hid8"]
         late = self.res_mode != "epi"
+        rs = self.rowsums and not late and all(lin.groupsize in (-1, lin.infeatures)
+                                               for lin in (p.qkv, p.lin1, p.lin2))
+        rs_x, rs_h = (bufs["rs_x"], bufs["rs_h"]) if rs else (None, None)
         if late and not first:
             ops.add_layernorm(x, self._delta(bufs, torch.float32), p.ln1_w, p.ln1_b, p.ln1_eps, out=xn8,
                               out_scale=p.s_qkv)
         else:
-            ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8, rows_per_wave=self.ln_rpw)
+            ops.layernorm_q(x, p.ln1_w, p.ln1_b, p.ln1_eps, out_scale=p.s_qkv, out=xn8, rows_per_wave=self.ln_rpw,
+                            rowsum=rs_x)
         mark(0)
-        p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv)
+        p.qkv.forward_w4a8(xn8, p.s_qkv, ops.EPI_BIAS, out=qkv, rowsum=rs_x)
         mark(1)
         if ("win" if p.window else "glob") not in self.skip:
             ops.rel_attention(qkv, p.qkv_bias, p.relh, p.relw, p.heads, p.window, p.scale, out=att8,
@@ -228,14 +239,15 @@ class EncoderEngine:
         else:
             p.proj.forward_w4a8(att8, p.s_proj, ops.EPI_RESADD_F32, out=x)
             mark(3)
-            ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8, rows_per_wave=self.ln_rpw)
+            ops.layernorm_q(x, p.ln2_w, p.ln2_b, p.ln2_eps, out_scale=p.s_lin1, out=xn8, rows_per_wave=self.ln_rpw,
+                            rowsum=rs_x, zero_rows=rs_h)
         mark(4)
-        p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2)
+        p.lin1.forward_w4a8(xn8, p.s_lin1, ops.EPI_Q8_GELU, out=hid8, out_scale=p.s_lin2, rowsum=rs_x, rowsum_out=rs_h)
         mark(5)
         if late and not last:
             p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_F32, out=self._delta(bufs, torch.float32))
         else:
-            p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x)
+            p.lin2.forward_w4a8(hid8, p.s_lin2, ops.EPI_RESADD_F32, out=x, rowsum=rs_h)
         mark(6)
 
     # ---------------------------------------------------------------- LayerNorm fold

@@ -350,10 +350,15 @@ def minmax_update(x2d: torch.Tensor, axis: int, max_val: Optional[torch.Tensor] 
 
 def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, in_scale: float = 0.0,
                 out_scale: float = 0.0, out_dtype: torch.dtype = torch.int8,
-                out: Optional[torch.Tensor] = None, rows_per_wave: int = 0) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, rows_per_wave: int = 0,
+                rowsum: Optional[torch.Tensor] = None, zero_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """LayerNorm with int8 codes on either side: x int8 (codes * in_scale) / f32 / f16;
     out int8 codes (q(y, out_scale)), f32 fake-quant (out_dtype f32 with out_scale > 0), f16 or f32.
-    ``rows_per_wave`` (1, 2, 4; 0 = library default) as in ``layernorm``."""
+    ``rows_per_wave`` (1, 2, 4; 0 = library default) as in ``layernorm``.  ``rowsum`` (int32 [rows],
+    int8-code output only): the output rows' code sums (``samq_layernorm_q_rs``, the W4A8 GEMM's
+    row sums); ``zero_rows`` (int32 [rows]) is zeroed on the way."""
+    if rowsum is not None:
+        return _layernorm_q_rs(x, gamma, beta, eps, in_scale, out_scale, out, rows_per_wave, rowsum, zero_rows)
     _need_cuda(x, gamma, beta)
     c = x.shape[-1]
     assert x.is_contiguous() and gamma.dtype == torch.float32 and beta.dtype == torch.float32
@@ -372,6 +377,32 @@ def layernorm_q(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: f
     _lib.check(_lib.load().samq_layernorm_q(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), x.numel() // c, c,
                                             float(eps), flags, float(in_scale), float(out_scale), _stream()),
                "layernorm_q")
+    return out
+
+
+def _rows_i32(t: Optional[torch.Tensor], rows: int, what: str) -> None:
+    if t is not None:
+        assert t.dtype == torch.int32 and t.is_contiguous() and t.numel() >= rows, f"{what}: int32 [rows] expected"
+
+
+def _layernorm_q_rs(x, gamma, beta, eps, in_scale, out_scale, out, rows_per_wave, rowsum, zero_rows):
+    _need_cuda(x, gamma, beta, rowsum, zero_rows)
+    c = x.shape[-1]
+    rows = x.numel() // c
+    assert x.is_contiguous() and gamma.dtype == torch.float32 and beta.dtype == torch.float32
+    _rows_i32(rowsum, rows, "layernorm_q rowsum")
+    _rows_i32(zero_rows, rows, "layernorm_q zero_rows")
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.int8, device=x.device)
+    assert out.dtype == torch.int8, "layernorm_q: row sums need int8-code output"
+    flags = _lib.LN_OUT_I8 | (rows_per_wave << 16)
+    if x.dtype == torch.int8:
+        flags |= _lib.LN_IN_I8
+    elif x.dtype == torch.float16:
+        flags |= _lib.LN_IN_F16
+    _lib.check(_lib.load().samq_layernorm_q_rs(_ptr(x), _ptr(out), _ptr(gamma), _ptr(beta), rows, c, float(eps), flags,
+                                               float(in_scale), float(out_scale), _ptr(rowsum), _ptr(zero_rows),
+                                               _stream()), "layernorm_q_rs")
     return out
 
 
@@ -452,10 +483,28 @@ def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: to
 
 
 def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_scale=1.0, out_scale=0.0,
-              out=None, groupsize=-1, cfg=0):
+              out=None, groupsize=-1, cfg=0, rowsum=None, rowsum_out=None):
     """GPTQ int4 weights (repacked layout 3) x int8 activation codes (cfg 0 = library pick).
     ``groupsize`` -1 (per-channel, ``wscale`` f32 [N]) or a multiple of 128 (grouped:
-    ``wscale`` f32 [G, N], ``qzeros`` [G, N/8]; samq_w4a8_gemm_cfg)."""
+    ``wscale`` f32 [G, N], ``qzeros`` [G, N/8]; samq_w4a8_gemm_cfg).  Per-channel only:
+    ``rowsum`` (int32 [M]) = the input rows' code sums from their producer (the zero-point
+    ping-pong then skips its own), ``rowsum_out`` (int32 [M], zeroed by the caller; int8-code
+    epilogues) accumulates the output rows' code sums (``samq_w4a8_gemm_rs``)."""
+    if (rowsum is not None or rowsum_out is not None) and groupsize in (-1, a.shape[-1]):
+        _need_cuda(a, wpacked3, wscale, bias, qzeros, rowsum, rowsum_out)
+        assert a.dtype == torch.int8 and wscale.dtype == torch.float32
+        assert bias is None or bias.dtype == torch.float32
+        k = a.shape[-1]
+        a2 = a.reshape(-1, k)
+        _rows_i32(rowsum, a2.shape[0], "w4a8_gemm rowsum")
+        _rows_i32(rowsum_out, a2.shape[0], "w4a8_gemm rowsum_out")
+        out, o2 = _i8_out(a2, n, epilogue, out, tuple(a.shape[:-1]))
+        status = _lib.load().samq_w4a8_gemm_rs(
+            _ptr(a2), a2.stride(0), _ptr(wpacked3), _ptr(wscale), _ptr(qzeros), _ptr(bias), _ptr(o2), o2.stride(0),
+            a2.shape[0], n, k, epilogue, float(a_scale), float(out_scale), _ptr(rowsum), _ptr(rowsum_out), cfg,
+            _stream())
+        _lib.check(status, "w4a8_gemm_rs")
+        return out
     if groupsize in (-1, a.shape[-1]):
         return i8_gemm(a, _lib.BF_W4, wpacked3, wscale, n, bias, qzeros, epilogue, a_scale, out_scale, out=out,
                        cfg=cfg)

@@ -111,12 +111,15 @@ class QuantLinear(nn.Module):
         return float(sc.reshape(-1)[0])
 
     def forward_w4a8(self, codes: torch.Tensor, a_scale: float, epilogue: int, out: Optional[torch.Tensor] = None,
-                     out_scale: float = 0.0) -> torch.Tensor:
-        """int8 input codes (scale ``a_scale``) x int4 weights on the int8 MFMA."""
+                     out_scale: float = 0.0, rowsum: Optional[torch.Tensor] = None,
+                     rowsum_out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """int8 input codes (scale ``a_scale``) x int4 weights on the int8 MFMA.  Per-channel weights:
+        ``rowsum`` / ``rowsum_out`` = the input / output rows' code sums (``ops.w4a8_gemm``)."""
         w = self.prepare_w4a8()
         gs = -1 if self.groupsize == self.infeatures else self.groupsize
         return ops.w4a8_gemm(codes, w["packed"], w["scale"], self.qzeros, self.outfeatures, w["bias"], epilogue,
-                             a_scale, out_scale, out=out, groupsize=gs, cfg=getattr(self, "i8_cfg", 0))
+                             a_scale, out_scale, out=out, groupsize=gs, cfg=getattr(self, "i8_cfg", 0),
+                             rowsum=rowsum, rowsum_out=rowsum_out)
 
     def forward_lnf(self, x: torch.Tensor, epilogue: int, out: torch.Tensor, stats: torch.Tensor, mu: torch.Tensor,
                     **kw) -> torch.Tensor:

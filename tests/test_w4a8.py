@@ -143,6 +143,13 @@ def test_w4a8_lanes_bit_identical_b8(cuda):
         one = eng(x[i:i + 1], out_dtype=torch.float32)
         assert torch.equal(one[0], ref[i]), i
     assert torch.isfinite(ref).all()
+    # the zero-point row sums from the producers (LN-q, lin1's epilogue atomics; engine.rowsums,
+    # round 6) against every GEMM summing its own A rows: bit-identical, eager and captured
+    eng.rowsums = False
+    own = eng(x, out_dtype=torch.float32, lanes=2)
+    torch.cuda.synchronize()
+    assert torch.equal(own, ref)
+    eng.rowsums = True
 
 
 @pytest.mark.gpu

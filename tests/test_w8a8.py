@@ -249,6 +249,81 @@ def test_w4a8_pingpong_matches_v3(cuda, m, k, n, cfg):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n", [(300, 1280, 512), (8192, 1280, 1280), (520, 5120, 1280), (8192, 1280, 5120),
+                                   (77, 128, 256)])
+def test_w4a8_gemm_rowsums(cuda, m, k, n):
+    """Zero-point row sums from the producer (samq_w4a8_gemm_rs, round 6): with ``rowsum`` = the exact
+    int32 code sums of A the ping-pong GEMMs (cfg 86 / 93 and the automatic pick) give the same bits
+    as summing A themselves, on every epilogue; ``rowsum_out`` (int8-code epilogues, any tile
+    config) accumulates exactly the row sums of the codes written, on top of what the buffer held."""
+    from oracle import gptq_pack
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(m + 3 * k + n))
+    w = rng.standard_normal((n, k), dtype=np.float32) * np.float32(0.02)
+    w[7] = np.abs(w[7])
+    fake, s, z = gptq_pack.rtn_quantize_linear(w, -1)
+    qw, qz, sc = gptq_pack.pack_linear(fake, s, z, -1)
+    packed = ops.w4_repack(torch.from_numpy(qw).to(cuda), layout=3)
+    a_np = rng.integers(-128, 128, (m, k), dtype=np.int8)
+    a_np[:3] = 127
+    a_np[3:5] = -128
+    a = torch.from_numpy(a_np).to(cuda)
+    rs = a.to(torch.int32).sum(1, dtype=torch.int32).contiguous()
+    scf = torch.from_numpy(sc.astype(np.float32).reshape(-1)).to(cuda)
+    qzd = torch.from_numpy(qz).to(cuda)
+    bias = torch.from_numpy(rng.standard_normal(n, dtype=np.float32) * np.float32(0.02)).to(cuda)
+    cfgs = [0] + ([86, 93] if n % 256 == 0 else [])
+    for cfg in cfgs:
+        for epi, osc in ((ops.EPI_BIAS, 0.0), (ops.EPI_BIAS_GELU, 0.0), (ops.EPI_F32, 0.0), (ops.EPI_Q8, 0.05),
+                         (ops.EPI_Q8_GELU, 0.03)):
+            ref = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, 0.02, osc, cfg=cfg)
+            got = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, 0.02, osc, cfg=cfg, rowsum=rs)
+            assert torch.equal(got, ref), (cfg, epi)
+            if epi in (ops.EPI_Q8, ops.EPI_Q8_GELU):
+                acc = torch.full((m,), 5, dtype=torch.int32, device=cuda)
+                got2 = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, epi, 0.02, osc, cfg=cfg, rowsum_out=acc)
+                assert torch.equal(got2, ref)
+                assert torch.equal(acc, got2.to(torch.int32).sum(1, dtype=torch.int32) + 5), (cfg, epi)
+        res0 = torch.from_numpy(rng.standard_normal((m, n), dtype=np.float32)).to(cuda)
+        r1, r2 = res0.clone(), res0.clone()
+        ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_RESADD_F32, 0.02, out=r1, cfg=cfg)
+        ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_RESADD_F32, 0.02, out=r2, cfg=cfg, rowsum=rs)
+        assert torch.equal(r1, r2), cfg
+    if n % 256 == 0:   # the v3 kernels emit the same output sums
+        acc = torch.zeros((m,), dtype=torch.int32, device=cuda)
+        o3 = ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_Q8_GELU, 0.02, 0.03, cfg=81, rowsum_out=acc)
+        assert torch.equal(acc, o3.to(torch.int32).sum(1, dtype=torch.int32))
+    with pytest.raises(AssertionError):   # output row sums of a non-code epilogue
+        ops.w4a8_gemm(a, packed, scf, qzd, n, bias, ops.EPI_BIAS, 0.02, cfg=0,
+                      rowsum_out=torch.zeros((m,), dtype=torch.int32, device=cuda))
+
+
+@pytest.mark.gpu
+def test_layernorm_q_rowsums(cuda):
+    """LN-q with the output rows' code sums (samq_layernorm_q_rs): identical codes to samq_layernorm_q,
+    rowsum = the exact int32 sum of each row's codes, zero_rows cleared; every rows-per-wave form
+    and a ragged row count, ViT-H width."""
+    from samq import ops
+    rng = np.random.Generator(np.random.PCG64(11))
+    rows, c = 1027, 1280
+    x = torch.from_numpy(rng.standard_normal((rows, c), dtype=np.float32) * 2).to(cuda)
+    g = torch.from_numpy((1 + 0.1 * rng.standard_normal(c)).astype(np.float32)).to(cuda)
+    b = torch.from_numpy((0.1 * rng.standard_normal(c)).astype(np.float32)).to(cuda)
+    ref = ops.layernorm_q(x, g, b, 1e-6, out_scale=0.021)
+    for rpw in (0, 1, 2, 4):
+        rs = torch.full((rows,), 3, dtype=torch.int32, device=cuda)
+        zr = torch.full((rows,), 9, dtype=torch.int32, device=cuda)
+        out = ops.layernorm_q(x, g, b, 1e-6, out_scale=0.021, rows_per_wave=rpw, rowsum=rs, zero_rows=zr)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), rpw
+        assert torch.equal(rs, ref.to(torch.int32).sum(1, dtype=torch.int32)), rpw
+        assert int(zr.abs().max()) == 0
+    rs = torch.zeros((rows,), dtype=torch.int32, device=cuda)
+    with pytest.raises(AssertionError):
+        ops.layernorm_q(x, g, b, 1e-6, out_scale=0.0, rowsum=rs)
+
+
+@pytest.mark.gpu
 def test_quantize_and_layernorm_q(cuda):
     from samq import ops
     rng = np.random.Generator(np.random.PCG64(3))

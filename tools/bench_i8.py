@@ -3,6 +3,7 @@ on the ViT-H projection shapes, with HIP events on the launch stream; outputs ch
 cfg 82 (int32-exact sums: every config must agree bit for bit).
 
     python tools/bench_i8.py [--m 16384,32768] [--cfgs 81,82,83]
+(cfg 100 + c: tile config c with the zero-point row sums supplied by the producer, round 6)
 """
 import argparse
 import sys
@@ -47,7 +48,15 @@ def main():
             a = torch.randint(-127, 128, (m, k), device=dev, dtype=torch.int8)
             osc = 0.05 if epi == ops.EPI_Q8_GELU else 0.0
 
+            rs = a.to(torch.int32).sum(1, dtype=torch.int32)
+            rso = torch.zeros(m, device=dev, dtype=torch.int32)
+
             def run(c, out):
+                if c >= 100:   # cfg c - 100 with the producer-side row sums (round 6: samq_w4a8_gemm_rs;
+                    # lin1 also accumulates its output row sums, as in the engine)
+                    return ops.w4a8_gemm(a, wb["packed"], wb["scale"], q.qzeros, n, wb["bias"], epi, 0.02, osc,
+                                         out=out, cfg=c - 100, rowsum=rs,
+                                         rowsum_out=rso if epi == ops.EPI_Q8_GELU else None)
                 return ops.i8_gemm(a, _lib.BF_W4, wb["packed"], wb["scale"], n, wb["bias"], q.qzeros, epi,
                                    0.02, osc, out=out, cfg=c)
             if epi == ops.EPI_RESADD_F32:
