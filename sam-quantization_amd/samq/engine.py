@@ -63,7 +63,10 @@ class EncoderEngine:
         # input come from its producer -- LN-q for qkv / lin1, lin1's Q8_GELU epilogue (int32 atomics)
         # for lin2 -- instead of every column tile of the ping-pong GEMM re-summing its A rows;
         # bit-identical either way (an in-graph A/B knob)
-        self.rowsums = True
+        self.rowsums = True   # True, False, or "ln" (LN-q's sums only: lin2 sums its own rows)
+        # lanes > 1: lane 0's HIP stream at high priority (its workgroups dispatched first, the
+        # other lanes fill the CUs it leaves) -- an in-graph A/B knob, default off
+        self.lane_priority = 0
         # timing-only A/B knob (tools): launches to leave out of the W4A16 block ("ln", "win",
         # "glob") -- the output is wrong; the empty default runs everything
         self.skip = frozenset()
@@ -217,7 +220,8 @@ class EncoderEngine:
         late = self.res_mode != "epi"
         rs = self.rowsums and not late and all(lin.groupsize in (-1, lin.infeatures)
                                                for lin in (p.qkv, p.lin1, p.lin2))
-        rs_x, rs_h = (bufs["rs_x"], bufs["rs_h"]) if rs else (None, None)
+        rs_x = bufs["rs_x"] if rs else None
+        rs_h = bufs["rs_h"] if rs and self.rowsums != "ln" else None
         if late and not first:
             ops.add_layernorm(x, self._delta(bufs, torch.float32), p.ln1_w, p.ln1_b, p.ln1_eps, out=xn8,
                               out_scale=p.s_qkv)
@@ -419,10 +423,14 @@ class EncoderEngine:
         return out
 
     def _lane_streams(self, lanes: int):
-        ss = getattr(self, "_streams", None)
-        if ss is None or len(ss) < lanes:
-            ss = self._streams = [torch.cuda.Stream(device=self.device) for _ in range(lanes)]
-        return ss[:lanes]
+        cache = self.__dict__.setdefault("_streams", {})
+        ss = cache.get((lanes, self.lane_priority))
+        if ss is None:
+            hi = torch.cuda.Stream.priority_range()[1]   # the numerically lowest = highest priority
+            ss = cache[(lanes, self.lane_priority)] = [
+                torch.cuda.Stream(device=self.device, priority=hi if (self.lane_priority and i == 0) else 0)
+                for i in range(lanes)]
+        return ss
 
     def _forward(self, img: torch.Tensor, bufs, out_dtype, gate_event=None) -> torch.Tensor:
         self.embed(img, bufs["x"])

@@ -31,6 +31,7 @@ img = torch.randn((4, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float
 graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.ln_rpw = cfg.get("ln_rpw", 0)
+    eng.lane_priority = cfg.get("prio", 0)   # round 6: lane 0's stream at high priority
     eng.res_mode = cfg.get("res", "epi")   # where the proj / lin2 residual adds run (engine.res_mode)
     eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only: "skip_ln=1" etc.
     for p in eng.plans:

@@ -35,7 +35,8 @@ graphs, ref = {}, None
 for name, cfg in VARIANTS.items():
     eng.res_mode = cfg.get("res", "epi")
     eng.ln_rpw = cfg.get("ln_rpw", 0)
-    eng.rowsums = bool(cfg.get("rowsums", 1))   # round 6: producer-side zero-point row sums
+    eng.lane_priority = cfg.get("prio", 0)   # round 6: lane 0's stream at high priority
+    eng.rowsums = {0: False, 1: True, 2: "ln"}[cfg.get("rowsums", 1)]   # round 6: producer-side row sums
     eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only
     for p in eng.plans:
         for lay in ("qkv", "proj", "lin1", "lin2"):
