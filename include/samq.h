@@ -325,6 +325,14 @@ int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float*
                           const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads,
                           int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
                           float s_out, hipStream_t stream);
+/* samq_rel_attention_q8 over a range of the grid's rows (round 6: the W8A8 engine's two row lanes
+ * run one image as two concurrent kernel chains): global (window == 0, H == W == 64) -- the queries of
+ * grid rows [row0, row0 + rows) against all keys; windows -- the windows of rows [row0, row0 + rows),
+ * row0 a multiple of window and rows too unless the range ends at H.  rows < 0: the whole grid. */
+int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
+                               const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
+                               int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
+                               int row0, int rows, hipStream_t stream);
 
 /* ---------------------------------------------------------------- patch embedding / neck */
 

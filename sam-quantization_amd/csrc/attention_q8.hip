@@ -32,6 +32,8 @@ struct AttnQ8Params {
   const float* relw;        // [2S-1, 64] f32
   int8_t* out;              // [B, H, W, C] codes
   int B, H, W, heads, C, S, window, nwh, nww, L;
+  int row0;                 // row range (round 6, samq_rel_attention_q8_rows): global -- first query grid
+                            // row (grid z = rows); windows -- first window row (nwh = the range's rows)
   float qk_scale, s_qkv, s_a1, s_a2, s_out;
   float inv_a1, inv_a2, k2;   // 1/s_a1, 1/s_a2, s_a2*log2(e)
 };
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(64 * NWQ) void rel_attention_q8_kernel(AttnQ8Params
   if (p.window > 0) {
     const int per = p.nwh * p.nww;
     b = blockIdx.x / per;
-    wy = (blockIdx.x % per) / p.nww;
+    wy = p.row0 + (blockIdx.x % per) / p.nww;
     wx = blockIdx.x % p.nww;
   } else {
     b = blockIdx.x;
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   const int C = p.C;
   const int head = blockIdx.y;
   const int b = blockIdx.x;
-  const int qy = blockIdx.z;                    // query grid row of this workgroup
+  const int qy = p.row0 + blockIdx.z;           // query grid row of this workgroup
   const int lazyc = q8_ptab_lazy(p.k2);
   q8_ptab_fill<NT>(ptab, p.k2, lazyc, tid);     // visible after the first barrier below
   const int qx = wave * 16 + ql;
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
   const int head = blockIdx.y;
   const int per = p.nwh * p.nww;
   const int b = blockIdx.x / per;
-  const int wy = (blockIdx.x % per) / p.nww;
+  const int wy = p.row0 + (blockIdx.x % per) / p.nww;
   const int wx = blockIdx.x % p.nww;
   auto tok_ptr = [&](int ty, int tx, bool& inimg) -> const int8_t* {
     const int y = wy * SW + ty, x = wx * SW + tx;
@@ -778,10 +780,10 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
 
 using namespace samq;
 
-extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
-                                     const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
-                                     int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
-                                     hipStream_t stream) {
+extern "C" int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
+                                          const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads,
+                                          int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
+                                          float s_out, int row0, int rows, hipStream_t stream) {
   if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention_q8: null pointer");
   SAMQ_REQUIRE(hd == QD, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: head_dim must be 64");
@@ -790,6 +792,11 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
                "rel_attention_q8: scales must be > 0");
   SAMQ_REQUIRE(((uintptr_t)qkv & 15) == 0 && ((uintptr_t)out & 3) == 0, SAMQ_ERR_INVALID,
                "rel_attention_q8: qkv must be 16-byte aligned");
+  if (rows < 0) { row0 = 0; rows = H; }   // the whole grid
+  SAMQ_REQUIRE(row0 >= 0 && rows > 0 && row0 + rows <= H, SAMQ_ERR_INVALID, "rel_attention_q8: bad row range");
+  SAMQ_REQUIRE(window > 0 ? (row0 % window == 0 && (rows % window == 0 || row0 + rows == H))
+                          : (rows == H || H == 64), SAMQ_ERR_UNSUPPORTED,
+               "rel_attention_q8: a row range must cover whole windows (global: the 64 x 64 grid only)");
   AttnQ8Params p{};
   p.qkv = qkv; p.qkv_bias = qkv_bias; p.relh = rel_pos_h; p.relw = rel_pos_w; p.out = out;
   p.B = B; p.H = H; p.W = W; p.heads = heads; p.C = heads * hd;
@@ -800,7 +807,8 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
   if (window > 0) {
     SAMQ_REQUIRE(window <= 16, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: window must be <= 16");
     p.S = window; p.window = window;
-    p.nwh = (H + window - 1) / window; p.nww = (W + window - 1) / window;
+    p.nwh = (rows + window - 1) / window; p.nww = (W + window - 1) / window;
+    p.row0 = row0 / window;
     p.L = window * window;
     const dim3 grid(B * p.nwh * p.nww, heads, 1);
     if (window == 14) {   // SAM's 14 x 14 windows: key and query rows of 16 slots, half a window per workgroup
@@ -816,11 +824,20 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
     p.S = H; p.window = 0; p.nwh = p.nww = 1; p.L = H * W;
     constexpr int NWQ = 4;
     const dim3 grid(B, heads, (p.L + 16 * NWQ - 1) / (16 * NWQ));
+    p.row0 = row0;
     if (H == 64)   // one grid row of queries per workgroup (16 * NWQ == 64)
-      hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ>), grid, dim3(64 * NWQ), 0, stream, p);
+      hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ>), dim3(B, heads, rows), dim3(64 * NWQ), 0, stream, p);
     else
       hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, false>), grid, dim3(64 * NWQ), 0, stream, p);
   }
   SAMQ_LAUNCH_CHECK("rel_attention_q8 launch");
   return SAMQ_OK;
+}
+
+extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
+                                     const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
+                                     int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
+                                     hipStream_t stream) {
+  return samq_rel_attention_q8_rows(qkv, qkv_bias, rel_pos_h, rel_pos_w, out, B, H, W, heads, hd, window, sm_scale,
+                                    s_qkv, s_a1, s_a2, s_out, 0, -1, stream);
 }

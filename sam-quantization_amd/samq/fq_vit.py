@@ -702,6 +702,13 @@ class W8A8Engine:
         # in the W8A8 graph 1.6543 vs 1.6836 ms per image, bit-identical; the ViT-H W4A8 graph keeps
         # the library default (two: -2.2 % with one, profiles/r5_ln_rpw_ab.log)
         self.ln_rpw = 1
+        # row lanes (round 6): one image as two concurrent kernel chains over the token grid's rows
+        # (split on a window boundary: per-row LayerNorm / GEMMs / residual, whole windows), joined
+        # only around the global blocks' attention (every query reads every key) and for the neck's
+        # 3x3 conv.  At batch 1 the ~90 launches of a step are small and serial: the second chain
+        # fills the first's inter-kernel gaps and tails.  Bit-identical to one chain (per-row
+        # kernels, integer-exact GEMMs on any tile).  1 = one chain.
+        self.row_lanes = 2
         dev = enc.pos_embed.device
         if dev.type != "cuda":
             raise RuntimeError("W8A8 engine: move the encoder to the GPU first")
@@ -793,6 +800,10 @@ class W8A8Engine:
         tap("qact1", x.view(b, gh, gw, c), s_x)
         xn = torch.empty_like(x)
         ao = torch.empty_like(x)
+        split = self._row_split(gh)
+        if taps is None and split:
+            s_x = self._blocks_row_lanes(x, xn, ao, b, gh, gw, c, split)
+            return self._neck(x, s_x, b, gh, gw)
         for i, bl in enumerate(self.blocks):
             pre = f"blocks.{i}."
             g1, b1, e1 = bl["n1"]
@@ -816,6 +827,90 @@ class W8A8Engine:
                        res_scale=bl["s_x1"], out=x)
             s_x = bl["s_x2"]
             tap(pre + "qact4", x.view(b, gh, gw, c), s_x)
+        return self._neck(x, s_x, b, gh, gw)
+
+    def _row_split(self, gh: int) -> int:
+        """First grid row of the second row lane (0: one chain): the window boundary nearest the
+        middle, so every window lies in one lane."""
+        if self.row_lanes <= 1:
+            return 0
+        wins = {bl["window"] for bl in self.blocks if bl["window"] > 0}
+        step = max(wins) if wins else 1
+        if len(wins) > 1 or gh < 2 * step:
+            return 0
+        return max(step, round(gh / 2 / step) * step)
+
+    def _blocks_row_lanes(self, x, xn, ao, b, gh, gw, c, split):
+        """The blocks as two kernel chains on their own HIP streams, lane 0 on grid rows [0, split),
+        lane 1 on [split, gh) (every image of the batch: rows r of image i are token rows
+        i * gh * gw + r * gw ..).  Global blocks: both lanes' qkv rows complete before either lane's
+        attention (events), and a lane's next qkv GEMM waits for the other lane's global attention
+        (it reads those qkv rows).  Returns the final activation scale."""
+        ops = self.ops
+        if b != 1:
+            raise NotImplementedError("W8A8 row lanes: batch 1 (config 2); larger batches run one chain")
+        ranges = ((0, split), (split, gh))
+        cur = torch.cuda.current_stream()
+        streams = self._lane_streams()
+        for st in streams:
+            st.wait_stream(cur)
+        # every buffer the lanes share is allocated on the forking stream (stream-ordered reuse stays
+        # behind the join)
+        qkv_all = torch.empty((b * gh * gw, 3 * c), dtype=torch.int8, device=x.device)
+        hid = torch.empty((b * gh * gw, self.blocks[0]["lin1"]["n"]), dtype=torch.int8, device=x.device)
+        pending = [None, None]   # per lane: the other lane must wait for this event before its next qkv GEMM
+        s_x = self.s_x0
+        for i, bl in enumerate(self.blocks):
+            glob = bl["window"] == 0
+            ev_qkv = []
+            for li, (r0, r1) in enumerate(ranges):
+                t0, t1 = r0 * gw, r1 * gw
+                with torch.cuda.stream(streams[li]):
+                    if pending[1 - li] is not None:
+                        streams[li].wait_event(pending[1 - li])
+                    g1, b1, e1 = bl["n1"]
+                    ops.layernorm_q(x[t0:t1], g1, b1, e1, in_scale=s_x, out_scale=bl["s_ln1"], out=xn[t0:t1],
+                                    rows_per_wave=self.ln_rpw)
+                    self._gemm(xn[t0:t1], bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"], out=qkv_all[t0:t1])
+                    if glob:
+                        ev = torch.cuda.Event()
+                        ev.record(streams[li])
+                        ev_qkv.append(ev)
+            pending = [None, None]
+            qkv = qkv_all.view(b, gh, gw, 3 * c)
+            for li, (r0, r1) in enumerate(ranges):
+                t0, t1 = r0 * gw, r1 * gw
+                with torch.cuda.stream(streams[li]):
+                    if glob:
+                        streams[li].wait_event(ev_qkv[1 - li])
+                    ops.rel_attention_q8(qkv, bl["qkv_bias"], bl["relh"], bl["relw"], bl["heads"], bl["window"],
+                                         bl["scale"], bl["s_qkv"], bl["s_a1"], bl["s_a2"], bl["s_ao"],
+                                         out=ao.view(b, gh, gw, c), rows=(r0, r1 - r0))
+                    if glob:
+                        ev = torch.cuda.Event()
+                        ev.record(streams[li])
+                        pending[li] = ev
+                    self._gemm(ao[t0:t1], bl["proj"], ops.EPI_Q8_RES, bl["s_ao"], bl["s_x1"], mid=bl["s_proj"],
+                               res=x[t0:t1], res_scale=s_x, out=x[t0:t1])
+                    g2, b2, e2 = bl["n2"]
+                    ops.layernorm_q(x[t0:t1], g2, b2, e2, in_scale=bl["s_x1"], out_scale=bl["s_ln2"], out=xn[t0:t1],
+                                    rows_per_wave=self.ln_rpw)
+                    self._gemm(xn[t0:t1], bl["lin1"], ops.EPI_Q8_GELU, bl["s_ln2"], bl["s_h"], out=hid[t0:t1])
+                    self._gemm(hid[t0:t1], bl["lin2"], ops.EPI_Q8_RES, bl["s_h"], bl["s_x2"], mid=bl["s_l2"],
+                               res=x[t0:t1], res_scale=bl["s_x1"], out=x[t0:t1])
+            s_x = bl["s_x2"]
+        for st in streams:
+            cur.wait_stream(st)
+        return s_x
+
+    def _lane_streams(self):
+        ss = self.__dict__.get("_streams")
+        if ss is None:
+            ss = self._streams = [torch.cuda.Stream(device=self.dev) for _ in range(2)]
+        return ss
+
+    def _neck(self, x, s_x, b, gh, gw):
+        ops = self.ops
         sq = self.s_q
         y0 = self._gemm(x, self.neck0, ops.EPI_Q8, s_x, sq[0])
         y1 = ops.layernorm_q(y0, self.ln_n1[0], self.ln_n1[1], self.ln_n1[2], in_scale=sq[0], out_scale=sq[1])

@@ -526,8 +526,11 @@ def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_sc
 
 def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,
                      rel_pos_w: torch.Tensor, heads: int, window: int, sm_scale: float, s_qkv: float, s_a1: float,
-                     s_a2: float, s_out: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """W8A8 attention on int8 qkv codes (B, H, W, 3C) -> int8 output codes (B, H, W, C)."""
+                     s_a2: float, s_out: float, out: Optional[torch.Tensor] = None,
+                     rows: Optional[tuple] = None) -> torch.Tensor:
+    """W8A8 attention on int8 qkv codes (B, H, W, 3C) -> int8 output codes (B, H, W, C).
+    ``rows = (row0, n)``: only the queries (global) / windows (windowed) of grid rows
+    [row0, row0 + n) are computed (``samq_rel_attention_q8_rows``)."""
     _need_cuda(qkv, qkv_bias, rel_pos_h, rel_pos_w)
     b, h, w, c3 = qkv.shape
     c = c3 // 3
@@ -536,9 +539,10 @@ def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_po
     assert qkv_bias is None or qkv_bias.dtype == torch.float32
     if out is None:
         out = torch.empty((b, h, w, c), dtype=torch.int8, device=qkv.device)
-    _lib.check(_lib.load().samq_rel_attention_q8(
+    r0, nr = rows if rows is not None else (0, -1)
+    _lib.check(_lib.load().samq_rel_attention_q8_rows(
         _ptr(qkv), _ptr(qkv_bias), _ptr(rel_pos_h.contiguous()), _ptr(rel_pos_w.contiguous()), _ptr(out), b, h, w,
-        heads, c // heads, window, float(sm_scale), float(s_qkv), float(s_a1), float(s_a2), float(s_out), _stream()),
-        "rel_attention_q8")
+        heads, c // heads, window, float(sm_scale), float(s_qkv), float(s_a1), float(s_a2), float(s_out), int(r0),
+        int(nr), _stream()), "rel_attention_q8")
     return out
 

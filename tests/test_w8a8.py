@@ -408,6 +408,63 @@ def test_rel_attention_q8(cuda, b, hw, window):
     _codes_close(out.cpu().numpy(), ref, 5e-3, f"attention_q8 {b}x{hw} win {window}")
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [0, 14])
+def test_rel_attention_q8_rows(cuda, window):
+    """Row ranges of the W8A8 attention (samq_rel_attention_q8_rows, the row lanes' split): global --
+    the queries of grid rows [r0, r0 + n) against every key; windows -- whole window rows, the last
+    range running past the grid into the padded windows.  The union of the ranges gives the full
+    launch's codes bit for bit; a range that cuts a window is refused."""
+    from samq import ops
+    heads, d, hw = 2, 64, 64
+    c = heads * d
+    rng = np.random.Generator(np.random.PCG64(77 + window))
+    qkv = torch.from_numpy(rng.integers(-128, 128, (1, hw, hw, 3 * c), dtype=np.int8)).to(cuda)
+    side = window or hw
+    relh = torch.from_numpy((rng.standard_normal((2 * side - 1, d), dtype=np.float32) * 0.5)).to(cuda)
+    relw = torch.from_numpy((rng.standard_normal((2 * side - 1, d), dtype=np.float32) * 0.5)).to(cuda)
+    bias = torch.from_numpy((rng.standard_normal(3 * c, dtype=np.float32) * 0.3)).to(cuda)
+    args = (qkv, bias, relh, relw, heads, window, d ** -0.5, 0.02, 2.0 / 127.5, 6.0 / 127.5, 2.6 / 127.5)
+    full = ops.rel_attention_q8(*args)
+    splits = [(0, 28), (28, 36)] if window else [(0, 28), (28, 36), (0, 1), (63, 1)]
+    out = torch.zeros_like(full)
+    for r0, n in splits[:2]:
+        ops.rel_attention_q8(*args, out=out, rows=(r0, n))
+    torch.cuda.synchronize()
+    assert torch.equal(out, full)
+    if not window:
+        for r0, n in splits[2:]:
+            one = torch.zeros_like(full)
+            ops.rel_attention_q8(*args, out=one, rows=(r0, n))
+            assert torch.equal(one[:, r0:r0 + n], full[:, r0:r0 + n]) and int(one[:, :r0].abs().sum()) == 0
+    else:
+        with pytest.raises(NotImplementedError):
+            ops.rel_attention_q8(*args, out=out, rows=(20, 14))
+
+
+@pytest.mark.gpu
+def test_w8a8_row_lanes_bit_identical(cuda):
+    """Config 2 geometry (vit_b W8A8, 1024^2, B = 1): the engine's two row lanes (grid rows [0, 28)
+    and [28, 64) as concurrent kernel chains, joined around the global blocks' attention) give the
+    one-chain output bit for bit, eager and as a captured HIP graph replayed twice."""
+    from samq.synthetic import random_fq_encoder
+    enc = random_fq_encoder("vit_b", device=cuda)
+    eng = enc.engine()
+    img = torch.randn((1, 3, 1024, 1024), generator=torch.Generator(device=cuda).manual_seed(5), device=cuda)
+    eng.row_lanes = 1
+    ref = eng(img).clone()
+    eng.row_lanes = 2
+    assert eng._row_split(64) == 28
+    got = eng(img)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    graph, gout = eng.capture(img)
+    for _ in range(2):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gout, ref)
+
+
 # ----------------------------------------------------------------------------- GPU: encoder
 def _gpu_fq(cfg, st, g, device):
     from samq import fq_vit

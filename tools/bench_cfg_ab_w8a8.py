@@ -26,8 +26,10 @@ eng = enc.engine()
 g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((1, 3, 1024, 1024), generator=g, device=dev)
 graphs, ref = {}, None
+rpw0, lanes0 = eng.ln_rpw, eng.row_lanes   # the engine's defaults are "pick"
 for name, cfg in VARIANTS.items():
-    eng.ln_rpw = cfg.get("ln_rpw", 0)
+    eng.ln_rpw = cfg.get("ln_rpw", rpw0)
+    eng.row_lanes = cfg.get("lanes", lanes0)   # round 6: one image as two row lanes
     for bl in eng.blocks:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             bl[lay]["cfg"] = cfg.get(lay, 0)
