@@ -842,54 +842,51 @@ class W8A8Engine:
 
     def _blocks_row_lanes(self, x, xn, ao, b, gh, gw, c, split):
         """The blocks as two kernel chains on their own HIP streams, lane 0 on grid rows [0, split),
-        lane 1 on [split, gh) (every image of the batch: rows r of image i are token rows
-        i * gh * gw + r * gw ..).  Global blocks: both lanes' qkv rows complete before either lane's
-        attention (events), and a lane's next qkv GEMM waits for the other lane's global attention
-        (it reads those qkv rows).  Returns the final activation scale."""
+        lane 1 on [split, gh).  Global blocks: both lanes' qkv rows are complete before either lane's
+        attention reads every key, and neither lane's next qkv GEMM overwrites its rows before the
+        other lane's global attention has read them -- two joins of the lanes through the forking
+        stream.  (Pairwise cross-stream events in place of the joins crashed the HIP graph capture,
+        tools/w8a8_lane_capture_probe.py.)  Returns the final activation scale."""
         ops = self.ops
         if b != 1:
             raise NotImplementedError("W8A8 row lanes: batch 1 (config 2); larger batches run one chain")
         ranges = ((0, split), (split, gh))
         cur = torch.cuda.current_stream()
         streams = self._lane_streams()
+
+        def join():   # the lanes wait for each other, through the forking stream
+            for st in streams:
+                cur.wait_stream(st)
+            for st in streams:
+                st.wait_stream(cur)
         for st in streams:
             st.wait_stream(cur)
         # every buffer the lanes share is allocated on the forking stream (stream-ordered reuse stays
-        # behind the join)
+        # behind the final join)
         qkv_all = torch.empty((b * gh * gw, 3 * c), dtype=torch.int8, device=x.device)
         hid = torch.empty((b * gh * gw, self.blocks[0]["lin1"]["n"]), dtype=torch.int8, device=x.device)
-        pending = [None, None]   # per lane: the other lane must wait for this event before its next qkv GEMM
+        qkv = qkv_all.view(b, gh, gw, 3 * c)
+        after_global = False
         s_x = self.s_x0
-        for i, bl in enumerate(self.blocks):
+        for bl in self.blocks:
             glob = bl["window"] == 0
-            ev_qkv = []
+            if after_global:
+                join()   # the previous global attention has read both lanes' qkv rows
             for li, (r0, r1) in enumerate(ranges):
                 t0, t1 = r0 * gw, r1 * gw
                 with torch.cuda.stream(streams[li]):
-                    if pending[1 - li] is not None:
-                        streams[li].wait_event(pending[1 - li])
                     g1, b1, e1 = bl["n1"]
                     ops.layernorm_q(x[t0:t1], g1, b1, e1, in_scale=s_x, out_scale=bl["s_ln1"], out=xn[t0:t1],
                                     rows_per_wave=self.ln_rpw)
                     self._gemm(xn[t0:t1], bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"], out=qkv_all[t0:t1])
-                    if glob:
-                        ev = torch.cuda.Event()
-                        ev.record(streams[li])
-                        ev_qkv.append(ev)
-            pending = [None, None]
-            qkv = qkv_all.view(b, gh, gw, 3 * c)
+            if glob:
+                join()   # every key row is projected before any query reads it
             for li, (r0, r1) in enumerate(ranges):
                 t0, t1 = r0 * gw, r1 * gw
                 with torch.cuda.stream(streams[li]):
-                    if glob:
-                        streams[li].wait_event(ev_qkv[1 - li])
                     ops.rel_attention_q8(qkv, bl["qkv_bias"], bl["relh"], bl["relw"], bl["heads"], bl["window"],
                                          bl["scale"], bl["s_qkv"], bl["s_a1"], bl["s_a2"], bl["s_ao"],
                                          out=ao.view(b, gh, gw, c), rows=(r0, r1 - r0))
-                    if glob:
-                        ev = torch.cuda.Event()
-                        ev.record(streams[li])
-                        pending[li] = ev
                     self._gemm(ao[t0:t1], bl["proj"], ops.EPI_Q8_RES, bl["s_ao"], bl["s_x1"], mid=bl["s_proj"],
                                res=x[t0:t1], res_scale=s_x, out=x[t0:t1])
                     g2, b2, e2 = bl["n2"]
@@ -898,6 +895,7 @@ class W8A8Engine:
                     self._gemm(xn[t0:t1], bl["lin1"], ops.EPI_Q8_GELU, bl["s_ln2"], bl["s_h"], out=hid[t0:t1])
                     self._gemm(hid[t0:t1], bl["lin2"], ops.EPI_Q8_RES, bl["s_h"], bl["s_x2"], mid=bl["s_l2"],
                                res=x[t0:t1], res_scale=bl["s_x1"], out=x[t0:t1])
+            after_global = glob
             s_x = bl["s_x2"]
         for st in streams:
             cur.wait_stream(st)
