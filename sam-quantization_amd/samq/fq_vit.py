@@ -702,13 +702,14 @@ class W8A8Engine:
         # in the W8A8 graph 1.6543 vs 1.6836 ms per image, bit-identical; the ViT-H W4A8 graph keeps
         # the library default (two: -2.2 % with one, profiles/r5_ln_rpw_ab.log)
         self.ln_rpw = 1
-        # row lanes (round 6): one image as two concurrent kernel chains over the token grid's rows
-        # (split on a window boundary: per-row LayerNorm / GEMMs / residual, whole windows), joined
-        # only around the global blocks' attention (every query reads every key) and for the neck's
-        # 3x3 conv.  At batch 1 the ~90 launches of a step are small and serial: the second chain
-        # fills the first's inter-kernel gaps and tails.  Bit-identical to one chain (per-row
-        # kernels, integer-exact GEMMs on any tile).  1 = one chain.
-        self.row_lanes = 2
+        # row lanes (round 6, opt-in): one image as two concurrent kernel chains over the token grid's
+        # rows (split on a window boundary: per-row LayerNorm / GEMMs / residual, whole windows),
+        # joined around the global blocks' attention (every query reads every key); the neck's 3x3
+        # conv after the final join.  Bit-identical to one chain (per-row kernels, integer-exact
+        # GEMMs on any tile).  Measured SLOWER in the W8A8 graph: 1.826 vs 1.664 ms per image
+        # (profiles/r6_w8a8_row_lanes.log) -- the step is not made of inter-kernel gaps that a
+        # second chain could fill; halving every launch costs more.  1 = one chain (default).
+        self.row_lanes = 1
         dev = enc.pos_embed.device
         if dev.type != "cuda":
             raise RuntimeError("W8A8 engine: move the encoder to the GPU first")

@@ -444,9 +444,9 @@ def test_rel_attention_q8_rows(cuda, window):
 
 @pytest.mark.gpu
 def test_w8a8_row_lanes_bit_identical(cuda):
-    """Config 2 geometry (vit_b W8A8, 1024^2, B = 1): the engine's two row lanes (grid rows [0, 28)
-    and [28, 64) as concurrent kernel chains, joined around the global blocks' attention) give the
-    one-chain output bit for bit, eager and as a captured HIP graph replayed twice."""
+    """Config 2 geometry (vit_b W8A8, 1024^2, B = 1): the engine's opt-in row lanes (grid rows
+    [0, 28) and [28, 64) as concurrent kernel chains, joined around the global blocks' attention)
+    give the one-chain output bit for bit, eager and as a captured HIP graph replayed twice."""
     from samq.synthetic import random_fq_encoder
     enc = random_fq_encoder("vit_b", device=cuda)
     eng = enc.engine()
