@@ -1098,12 +1098,17 @@ static int launch_i8_cfg(const I8Args& a, int cfg, hipStream_t st) {
     case 90: return launch_i8<64, 128, 2, 2, EPI, BF, 2>(a, st);
     case 91: return launch_i8<32, 64, 1, 2, EPI, BF, 2>(a, st);
     case 92: return launch_i8<64, 32, 2, 1, EPI, BF, 2>(a, st);
+    // round 6: bigger tiles on a 2-stage ring for the L2-bound vit_b B = 1 shapes (each 64x64 tile
+    // re-reads its A and B panels from L2: 128x128 halves those bytes per output)
+    case 180: return launch_i8<128, 128, 2, 2, EPI, BF, 2>(a, st);   // 64 KiB: two workgroups per CU
+    case 181: return launch_i8<128, 64, 2, 2, EPI, BF, 2>(a, st);    // 48 KiB
+    case 182: return launch_i8<128, 128, 2, 4, EPI, BF, 2>(a, st);   // 8 waves of 64x32
     default: return fail(SAMQ_ERR_INVALID, "i8_gemm: unknown tile config");
   }
 }
 
 static int i8_cfg_bn(int cfg) {
-  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: case 99: return 128; case 84: case 87: case 89: case 91: return 64;
+  switch (cfg) { case 81: case 82: case 85: case 86: case 93: case 94: case 95: case 96: case 97: return 256; case 83: case 88: case 90: case 99: case 180: case 182: return 128; case 84: case 87: case 89: case 91: case 181: return 64;
     case 92: return 32; default: return 0; }
 }
 
