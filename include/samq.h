@@ -157,6 +157,13 @@ int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* wpacked, con
                        int K, int groupsize, int epilogue, float a_scale, float out_scale, int cfg,
                        hipStream_t stream);
 
+/* samq_w8a8_gemm with the Q8 epilogue (the fq_vit qkv QLinear + attn.qact1) that also stores the
+ * codes of output columns [v_col0, N) as fp16 values into v16 [M, ldv] (column c at c - v_col0): the V
+ * third of qkv for samq_rel_attention_q8_rows' v16 (round 6).  v_col0 % 64 == 0. */
+int samq_w8a8_gemm_v16(const int8_t* A, int64_t lda, const int8_t* wpacked, const float* wscale,
+                       const float* bias, int8_t* C, int64_t ldc, int M, int N, int K, float a_scale,
+                       float out_scale, void* v16, int v_col0, int64_t ldv, int cfg, hipStream_t stream);
+
 /* Per-channel W4A8 GEMM with the zero point's row sums moved to the producers (round 6):
  * rowsum_in (optional, int32 [M]) = S[m] = sum_k A[m, k] of the int8 input rows -- the zero-point
  * ping-pong (cfg 86 / 93) then subtracts zp[n] * S[m] without re-summing A per column tile; kernels
@@ -325,14 +332,16 @@ int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, const float*
                           const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads,
                           int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
                           float s_out, hipStream_t stream);
-/* samq_rel_attention_q8 over a range of the grid's rows (round 6: the W8A8 engine's two row lanes
+/* samq_rel_attention_q8 over a range of the grid's rows (round 6: the W8A8 engine's opt-in row lanes
  * run one image as two concurrent kernel chains): global (window == 0, H == W == 64) -- the queries of
  * grid rows [row0, row0 + rows) against all keys; windows -- the windows of rows [row0, row0 + rows),
- * row0 a multiple of window and rows too unless the range ends at H.  rows < 0: the whole grid. */
+ * row0 a multiple of window and rows too unless the range ends at H.  rows < 0: the whole grid.
+ * v16 (optional, 16-byte aligned): the V codes as fp16 [B, H, W, heads*hd] (samq_w8a8_gemm_v16) --
+ * the 64 x 64 global kernel then stages V without converting it; same output codes. */
 int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
                                const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads, int hd,
                                int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
-                               int row0, int rows, hipStream_t stream);
+                               int row0, int rows, const void* v16, hipStream_t stream);
 
 /* ---------------------------------------------------------------- patch embedding / neck */
 

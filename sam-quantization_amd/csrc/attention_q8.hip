@@ -32,6 +32,7 @@ struct AttnQ8Params {
   const float* relw;        // [2S-1, 64] f32
   int8_t* out;              // [B, H, W, C] codes
   int B, H, W, heads, C, S, window, nwh, nww, L;
+  const _Float16* v16;      // optional [B, H, W, C] fp16 copy of the V codes (samq_w8a8_gemm_v16)
   int row0;                 // row range (round 6, samq_rel_attention_q8_rows): global -- first query grid
                             // row (grid z = rows); windows -- first window row (nwh = the range's rows)
   float qk_scale, s_qkv, s_a1, s_a2, s_out;
@@ -390,7 +391,12 @@ __device__ __forceinline__ void q8_ptab_unpack(const uint32_t (&w)[8], half8_t& 
   blo = __builtin_bit_cast(half8_t, lo);
 }
 
-template <int NWQ>
+// V16 (round 6): V staged from the producer's fp16 copy (p.v16, two 16-byte pieces per thread and
+// key row, no int8 -> fp16 conversion: 28 of the loop's 252 VALU per wave and key row).  Score codes
+// (round 6): the second quantiser rounds by adding 1.5 * 2^23 (exact round-half-even for |x| < 2^22)
+// and clamps in that biased form, so a code's P-table address is one v_lshl_add of its bits -- no
+// float -> int conversion per score.
+template <int NWQ, bool V16 = false>
 __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(AttnQ8Params p) {
   constexpr int G = 64, KC = 64, VP = QD + 8;    // V row pitch (halves): spreads the tr reads over banks
   constexpr int NT = 64 * NWQ;
@@ -421,14 +427,21 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   // ---- K / V staging: piece u = key * 4 + part (16 bytes of dims 16 part .. +15).  Two register
   // sets: chunk ch + 2 is loaded while chunk ch is computed and chunk ch + 1 (loaded one chunk
   // earlier) is stored -- two chunks of math to cover each load's latency
-  u32x4 kreg[2][UPT], vreg[2][UPT];
+  u32x4 kreg[2][UPT], vreg[2][V16 ? 2 * UPT : UPT];
+  const _Float16* v16img = V16 ? p.v16 + (int64_t)b * G * G * C : nullptr;
   auto load = [&](int kh, int r) {
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const int u = tid + j * NT, key = u >> 2, part = u & 3;
       const int8_t* tp = img + ((int64_t)kh * G + key) * ts + head * QD + part * 16;
       kreg[r][j] = *(const u32x4*)(tp + C);
-      vreg[r][j] = *(const u32x4*)(tp + 2 * C);
+      if constexpr (V16) {
+        const _Float16* vp = v16img + ((int64_t)kh * G + key) * C + head * QD + part * 16;
+        vreg[r][2 * j] = *(const u32x4*)vp;
+        vreg[r][2 * j + 1] = *(const u32x4*)(vp + 8);
+      } else {
+        vreg[r][j] = *(const u32x4*)(tp + 2 * C);
+      }
     }
   };
   auto store = [&](int buf, int r) {
@@ -436,14 +449,19 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
     for (int j = 0; j < UPT; ++j) {
       const int u = tid + j * NT, key = u >> 2, part = u & 3;
       *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kreg[r][j];
-      half8_t h0, h1;
+      if constexpr (V16) {
+        *(u32x4*)(&v_lds[buf][key * VP + part * 16]) = vreg[r][2 * j];
+        *(u32x4*)(&v_lds[buf][key * VP + part * 16 + 8]) = vreg[r][2 * j + 1];
+      } else {
+        half8_t h0, h1;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        h0[e] = (_Float16)(float)(int8_t)((vreg[r][j][e >> 2] >> (8 * (e & 3))) & 0xFFu);
-        h1[e] = (_Float16)(float)(int8_t)((vreg[r][j][2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
+        for (int e = 0; e < 8; ++e) {
+          h0[e] = (_Float16)(float)(int8_t)((vreg[r][j][e >> 2] >> (8 * (e & 3))) & 0xFFu);
+          h1[e] = (_Float16)(float)(int8_t)((vreg[r][j][2 + (e >> 2)] >> (8 * (e & 3))) & 0xFFu);
+        }
+        *(half8_t*)(&v_lds[buf][key * VP + part * 16]) = h0;
+        *(half8_t*)(&v_lds[buf][key * VP + part * 16 + 8]) = h1;
       }
-      *(half8_t*)(&v_lds[buf][key * VP + part * 16]) = h0;
-      *(half8_t*)(&v_lds[buf][key * VP + part * 16 + 8]) = h1;
     }
   };
   load(0, 0);
@@ -485,8 +503,15 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   const float lazy = (float)lazyc;
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
+  // score codes in the biased form y = MAG + c (MAG = 1.5 * 2^23: the add rounds half-even, the
+  // bits of y are MAGB + c); m is kept in the same form
+  constexpr float MAG = 12582912.0f;
+  constexpr int MAGB = 0x4B400000;
   float m = -INFINITY;
-  int pofs = 0;   // 256 - m: the table index of code c is c + pofs
+  // LDS byte address of the P-table entry of code y: (bits(y) << 2) + tbase, tbase = ptab + 4 (256 -
+  // m_code - MAGB) (mod 2^32)
+  uint32_t tbase = 0;
+  const uint32_t ptab_addr = (uint32_t)(uintptr_t)(SAMQ_LDS void*)ptab;
   float4_t acc[QD / 16], lacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -496,7 +521,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
     const int buf = ch & 1;
     load(ch + 2 < G ? ch + 2 : G - 1, buf);      // register set of chunk ch (stored one chunk ago);
                                                 // unconditional (clamped) so the waits stay counted
-    // ---- scores -> two quantisers -> integer codes c
+    // ---- scores -> two quantisers -> integer codes, biased (y = MAG + c)
     const float rh_row = rhq[ch] * inv2;
     float c[4][4];
 #pragma unroll
@@ -507,7 +532,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float q1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f);
-        c[bb][i] = __builtin_amdgcn_fmed3f(__builtin_rintf(fmaf(q1, k12, rh_row + rwr[bb][i])), -128.f, 127.f);
+        c[bb][i] = __builtin_amdgcn_fmed3f(fmaf(q1, k12, rh_row + rwr[bb][i]) + MAG, MAG - 128.f, MAG + 127.f);
       }
     }
     float cmax = q8max3(c[0][0], c[0][1], c[0][2]);
@@ -525,12 +550,15 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       lacc = lacc * alpha;
       m = cmax;
-      pofs = 256 - (int)cmax;
+      tbase = ptab_addr + 4u * (uint32_t)(256 - (__builtin_bit_cast(int, cmax) - MAGB) - MAGB);
     }
     // ---- P (hi + lo fp16, from the table) and O^T += V^T.P^T, l += ones.P^T, two 32-key steps
     uint32_t pw[2][8];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) pw[j >> 3][j & 7] = ptab[(int)c[j >> 2][j & 3] + pofs];
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t a = ((uint32_t)__builtin_bit_cast(int, c[j >> 2][j & 3]) << 2) + tbase;
+      pw[j >> 3][j & 7] = *(const SAMQ_LDS uint32_t*)(uintptr_t)a;
+    }
     const _Float16* vb = &v_lds[buf][0];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -783,7 +811,7 @@ using namespace samq;
 extern "C" int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bias, const float* rel_pos_h,
                                           const float* rel_pos_w, int8_t* out, int B, int H, int W, int heads,
                                           int hd, int window, float sm_scale, float s_qkv, float s_a1, float s_a2,
-                                          float s_out, int row0, int rows, hipStream_t stream) {
+                                          float s_out, int row0, int rows, const void* v16, hipStream_t stream) {
   if (B == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
   SAMQ_REQUIRE(qkv && rel_pos_h && rel_pos_w && out, SAMQ_ERR_INVALID, "rel_attention_q8: null pointer");
   SAMQ_REQUIRE(hd == QD, SAMQ_ERR_UNSUPPORTED, "rel_attention_q8: head_dim must be 64");
@@ -797,8 +825,10 @@ extern "C" int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bi
   SAMQ_REQUIRE(window > 0 ? (row0 % window == 0 && (rows % window == 0 || row0 + rows == H))
                           : (rows == H || H == 64), SAMQ_ERR_UNSUPPORTED,
                "rel_attention_q8: a row range must cover whole windows (global: the 64 x 64 grid only)");
+  SAMQ_REQUIRE(((uintptr_t)v16 & 15) == 0, SAMQ_ERR_INVALID, "rel_attention_q8: v16 must be 16-byte aligned");
   AttnQ8Params p{};
   p.qkv = qkv; p.qkv_bias = qkv_bias; p.relh = rel_pos_h; p.relw = rel_pos_w; p.out = out;
+  p.v16 = (const _Float16*)v16;
   p.B = B; p.H = H; p.W = W; p.heads = heads; p.C = heads * hd;
   // (q * scale) . k with q = c_q * s_qkv, k = c_k * s_qkv  (fq_vit image_encoder.py:455)
   p.qk_scale = (s_qkv * sm_scale) * s_qkv;
@@ -826,7 +856,10 @@ extern "C" int samq_rel_attention_q8_rows(const int8_t* qkv, const float* qkv_bi
     const dim3 grid(B, heads, (p.L + 16 * NWQ - 1) / (16 * NWQ));
     p.row0 = row0;
     if (H == 64)   // one grid row of queries per workgroup (16 * NWQ == 64)
-      hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ>), dim3(B, heads, rows), dim3(64 * NWQ), 0, stream, p);
+    {
+      if (v16) hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ, true>), dim3(B, heads, rows), dim3(64 * NWQ), 0, stream, p);
+      else hipLaunchKernelGGL((rel_attention_q8_row64_kernel<NWQ>), dim3(B, heads, rows), dim3(64 * NWQ), 0, stream, p);
+    }
     else
       hipLaunchKernelGGL((rel_attention_q8_kernel<false, NWQ, 64, 64, false>), grid, dim3(64 * NWQ), 0, stream, p);
   }
@@ -839,5 +872,5 @@ extern "C" int samq_rel_attention_q8(const int8_t* qkv, const float* qkv_bias, c
                                      int window, float sm_scale, float s_qkv, float s_a1, float s_a2, float s_out,
                                      hipStream_t stream) {
   return samq_rel_attention_q8_rows(qkv, qkv_bias, rel_pos_h, rel_pos_w, out, B, H, W, heads, hd, window, sm_scale,
-                                    s_qkv, s_a1, s_a2, s_out, 0, -1, stream);
+                                    s_qkv, s_a1, s_a2, s_out, 0, -1, nullptr, stream);
 }

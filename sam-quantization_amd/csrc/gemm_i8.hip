@@ -39,6 +39,12 @@ struct I8Epi {
   // with one int32 atomic per row and 16 x (WN / 16) codes -- the caller zeroes it first
   const int* rs_in;
   int* rs_out;
+  // Q8 epilogue (round 6, the W8A8 qkv GEMM): the codes of columns >= v16_col0 (the V third) are
+  // also stored as fp16 values (exact small integers) into v16 [rows, ldv] at column c - v16_col0,
+  // so the attention stages V without an int8 -> fp16 conversion per key row
+  _Float16* v16;
+  int v16_col0;
+  int64_t ldv;
 };
 
 // Implicit-GEMM A operand (AG != 0): the int8 codes are gathered from an image / feature map
@@ -207,6 +213,7 @@ __device__ __forceinline__ void i8_epilogue_slice(int i, const AccV (&acc)[TM][T
               res = *(const u32x4*)(ep_args.R + (int64_t)(ep_args.rmod > 0 ? row % ep_args.rmod : row) * ep_args.ldr +
                                     col_base + 16 * c16);
             u32x4 o;
+            float vq[EPI == SAMQ_EPI_Q8 ? 16 : 1];
 #pragma unroll
             for (int w = 0; w < 4; ++w) {
               float cq[4];
@@ -223,10 +230,27 @@ __device__ __forceinline__ void i8_epilogue_slice(int i, const AccV (&acc)[TM][T
                                                            : q8_exact2(x, ep_args.out_scale, inv_out, lim_out);
                 cq[b] = q.x;
                 cq[b + 1] = q.y;
+                if constexpr (EPI == SAMQ_EPI_Q8) {
+                  vq[4 * w + b] = q.x;
+                  vq[4 * w + b + 1] = q.y;
+                }
               }
               o[w] = q8_pack4(cq[0], cq[1], cq[2], cq[3]);
             }
             *(u32x4*)((int8_t*)Cout + (int64_t)row * ldc + col_base + 16 * c16) = o;
+            if constexpr (EPI == SAMQ_EPI_Q8) {
+              if (ep_args.v16 && col_base >= ep_args.v16_col0) {   // (uniform: a wave's columns are in one third)
+                half8_t h0, h1;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  h0[e] = (_Float16)vq[e];
+                  h1[e] = (_Float16)vq[8 + e];
+                }
+                _Float16* vp = ep_args.v16 + (int64_t)row * ep_args.ldv + (col_base - ep_args.v16_col0) + 16 * c16;
+                *(half8_t*)vp = h0;
+                *(half8_t*)(vp + 8) = h1;
+              }
+            }
             if (ep_args.rs_out) {
 #pragma unroll
               for (int w = 0; w < 4; ++w) rsum = __builtin_amdgcn_sdot4((int)o[w], 0x01010101, rsum, false);
@@ -1300,6 +1324,28 @@ extern "C" int samq_w4a8_gemm_cfg(const int8_t* A, int64_t lda, const int32_t* w
   I8Args a{A, lda, (const char*)wpacked, wscale, (const uint32_t*)qzeros, bias, C, ldc, M, N, K,
            I8Epi{a_scale, 0.f, 0.f, out_scale, nullptr, 0, 0, groupsize / 128}, I8Gather{0, 0, 0}};
   return i8_dispatch_grouped(a, epilogue, cfg, stream);
+}
+
+extern "C" int samq_w8a8_gemm_v16(const int8_t* A, int64_t lda, const int8_t* wpacked, const float* wscale,
+                                  const float* bias, int8_t* C, int64_t ldc, int M, int N, int K, float a_scale,
+                                  float out_scale, void* v16, int v_col0, int64_t ldv, int cfg, hipStream_t stream) {
+  if (M == 0) return SAMQ_OK;   // empty batch: no work, data pointers may be null
+  SAMQ_REQUIRE(A && wpacked && wscale && C && v16, SAMQ_ERR_INVALID, "w8a8_gemm_v16: null pointer");
+  SAMQ_REQUIRE(M > 0 && N > 0 && K > 0 && K % 128 == 0 && N % 64 == 0, SAMQ_ERR_INVALID,
+               "w8a8_gemm_v16: K % 128 == 0 and N % 64 == 0 required");
+  SAMQ_REQUIRE(lda >= K && lda % 16 == 0 && ((uintptr_t)A & 15) == 0 && ldc >= N && ldc % 16 == 0 &&
+               ((uintptr_t)C & 15) == 0, SAMQ_ERR_INVALID, "w8a8_gemm_v16: 16-byte aligned rows required");
+  SAMQ_REQUIRE(out_scale > 0.f, SAMQ_ERR_INVALID, "w8a8_gemm_v16: needs out_scale > 0");
+  if (cfg <= 0) cfg = i8_pick_cfg(M, N, BF_W8);
+  const int bn = i8_cfg_bn(cfg);
+  SAMQ_REQUIRE(bn > 0 && N % bn == 0, SAMQ_ERR_INVALID, "w8a8_gemm_v16: N not divisible by tile");
+  SAMQ_REQUIRE(v_col0 >= 0 && v_col0 < N && v_col0 % 64 == 0 && ldv >= N - v_col0 && ldv % 8 == 0 &&
+               ((uintptr_t)v16 & 15) == 0, SAMQ_ERR_INVALID,
+               "w8a8_gemm_v16: v_col0 must be a multiple of 64 inside N; v16 rows 16-byte aligned, ldv >= N - v_col0");
+  I8Args a{A, lda, (const char*)wpacked, wscale, nullptr, bias, C, ldc, M, N, K,
+           I8Epi{a_scale, 0.f, 0.f, out_scale, nullptr, 0, 0, 0, nullptr, nullptr, (_Float16*)v16, v_col0, ldv},
+           I8Gather{0, 0, 0}};
+  return launch_i8_cfg<SAMQ_EPI_Q8, BF_W8>(a, cfg, stream);
 }
 
 extern "C" int samq_w4a8_gemm_rs(const int8_t* A, int64_t lda, const int32_t* wpacked, const float* wscale,

@@ -92,7 +92,9 @@ SIGNATURES = {
     "samq_rel_attention_q8": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _f32,
                                      _f32, _f32, _f32, _vp]),
     "samq_rel_attention_q8_rows": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _f32, _f32,
-                                          _f32, _f32, _f32, _i32, _i32, _vp]),
+                                          _f32, _f32, _f32, _i32, _i32, _vp, _vp]),
+    "samq_w8a8_gemm_v16": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _f32, _f32, _vp, _i32, _i64,
+                                  _i32, _vp]),
     "samq_patch_embed": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_patch_embed_f32": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp]),
     "samq_patch_embed_u8": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _i32, _i32,

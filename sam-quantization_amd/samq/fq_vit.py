@@ -710,6 +710,9 @@ class W8A8Engine:
         # (profiles/r6_w8a8_row_lanes.log) -- the step is not made of inter-kernel gaps that a
         # second chain could fill; halving every launch costs more.  1 = one chain (default).
         self.row_lanes = 1
+        # global blocks (64 x 64 grid): the qkv GEMM also stores the V codes as fp16
+        # (samq_w8a8_gemm_v16) and the global attention stages them unconverted (round 6; same codes)
+        self.v16 = True
         dev = enc.pos_embed.device
         if dev.type != "cuda":
             raise RuntimeError("W8A8 engine: move the encoder to the GPU first")
@@ -801,6 +804,7 @@ class W8A8Engine:
         tap("qact1", x.view(b, gh, gw, c), s_x)
         xn = torch.empty_like(x)
         ao = torch.empty_like(x)
+        v16buf = None
         split = self._row_split(gh)
         if taps is None and split:
             s_x = self._blocks_row_lanes(x, xn, ao, b, gh, gw, c, split)
@@ -810,11 +814,20 @@ class W8A8Engine:
             g1, b1, e1 = bl["n1"]
             ops.layernorm_q(x, g1, b1, e1, in_scale=s_x, out_scale=bl["s_ln1"], out=xn, rows_per_wave=self.ln_rpw)
             tap(pre + "qact1", xn.view(b, gh, gw, c), bl["s_ln1"])
-            qkv = self._gemm(xn, bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"]).view(b, gh, gw, 3 * c)
+            v16 = None
+            if self.v16 and bl["window"] == 0 and gh == 64 and gw == 64:
+                # global block: the qkv GEMM also writes the V codes as fp16 for the attention's staging
+                if v16buf is None:
+                    v16buf = torch.empty((b, gh, gw, c), dtype=torch.float16, device=x.device)
+                v16 = v16buf
+                qkv = ops.w8a8_gemm_v16(xn, bl["qkv"]["packed"], bl["qkv"]["scale"], bl["qkv"]["n"], bl["qkv"]["bias"],
+                                        bl["s_ln1"], bl["s_qkv"], v16, 2 * c, cfg=bl["qkv"]["cfg"]).view(b, gh, gw, 3 * c)
+            else:
+                qkv = self._gemm(xn, bl["qkv"], ops.EPI_Q8, bl["s_ln1"], bl["s_qkv"]).view(b, gh, gw, 3 * c)
             tap(pre + "attn.qact1", qkv, bl["s_qkv"])
             ops.rel_attention_q8(qkv, bl["qkv_bias"], bl["relh"], bl["relw"], bl["heads"], bl["window"],
                                  bl["scale"], bl["s_qkv"], bl["s_a1"], bl["s_a2"], bl["s_ao"],
-                                 out=ao.view(b, gh, gw, c))
+                                 out=ao.view(b, gh, gw, c), v16=v16)
             tap(pre + "attn.qact2", ao.view(b, gh, gw, c), bl["s_ao"])
             self._gemm(ao, bl["proj"], ops.EPI_Q8_RES, bl["s_ao"], bl["s_x1"], mid=bl["s_proj"], res=x, res_scale=s_x,
                        out=x)

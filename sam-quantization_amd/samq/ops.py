@@ -459,6 +459,22 @@ def w8a8_gemm(a, wpacked, wscale, n, bias=None, epilogue=EPI_Q8, a_scale=1.0, ou
                    res_scale, res, out, cfg)
 
 
+def w8a8_gemm_v16(a, wpacked, wscale, n, bias, a_scale, out_scale, v16, v_col0, out=None, cfg=0):
+    """``w8a8_gemm`` with the Q8 epilogue that also stores the codes of columns [v_col0, n) as fp16
+    into ``v16`` (rows x (n - v_col0)): the fq_vit qkv projection feeding ``rel_attention_q8(v16=)``."""
+    _need_cuda(a, wpacked, wscale, bias, v16)
+    assert a.dtype == torch.int8 and wscale.dtype == torch.float32 and v16.dtype == torch.float16
+    k = a.shape[-1]
+    a2 = a.reshape(-1, k)
+    out, o2 = _i8_out(a2, n, EPI_Q8, out, tuple(a.shape[:-1]))
+    v2 = v16.reshape(a2.shape[0], -1)
+    assert v2.is_contiguous() and v2.shape[1] >= n - v_col0
+    _lib.check(_lib.load().samq_w8a8_gemm_v16(
+        _ptr(a2), a2.stride(0), _ptr(wpacked), _ptr(wscale), _ptr(bias), _ptr(o2), o2.stride(0), a2.shape[0], n, k,
+        float(a_scale), float(out_scale), _ptr(v2), int(v_col0), v2.stride(0), cfg, _stream()), "w8a8_gemm_v16")
+    return out
+
+
 def w8a8_conv_gemm(x: torch.Tensor, mode: int, wpacked: torch.Tensor, wscale: torch.Tensor, n: int,
                    bias: Optional[torch.Tensor] = None, epilogue: int = EPI_Q8, a_scale: float = 1.0,
                    out_scale: float = 0.0, mid_scale: float = 0.0, res_scale: float = 0.0,
@@ -527,10 +543,14 @@ def w4a8_gemm(a, wpacked3, wscale, qzeros, n, bias=None, epilogue=EPI_BIAS, a_sc
 def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_pos_h: torch.Tensor,
                      rel_pos_w: torch.Tensor, heads: int, window: int, sm_scale: float, s_qkv: float, s_a1: float,
                      s_a2: float, s_out: float, out: Optional[torch.Tensor] = None,
-                     rows: Optional[tuple] = None) -> torch.Tensor:
+                     rows: Optional[tuple] = None, v16: Optional[torch.Tensor] = None) -> torch.Tensor:
     """W8A8 attention on int8 qkv codes (B, H, W, 3C) -> int8 output codes (B, H, W, C).
     ``rows = (row0, n)``: only the queries (global) / windows (windowed) of grid rows
-    [row0, row0 + n) are computed (``samq_rel_attention_q8_rows``)."""
+    [row0, row0 + n) are computed (``samq_rel_attention_q8_rows``).  ``v16``: the V codes as fp16
+    (B, H, W, C) from ``w8a8_gemm_v16`` (the global kernel then stages V unconverted)."""
+    if v16 is not None:
+        _need_cuda(v16)
+        assert v16.dtype == torch.float16 and v16.is_contiguous() and v16.numel() == qkv.numel() // 3
     _need_cuda(qkv, qkv_bias, rel_pos_h, rel_pos_w)
     b, h, w, c3 = qkv.shape
     c = c3 // 3
@@ -543,6 +563,6 @@ def rel_attention_q8(qkv: torch.Tensor, qkv_bias: Optional[torch.Tensor], rel_po
     _lib.check(_lib.load().samq_rel_attention_q8_rows(
         _ptr(qkv), _ptr(qkv_bias), _ptr(rel_pos_h.contiguous()), _ptr(rel_pos_w.contiguous()), _ptr(out), b, h, w,
         heads, c // heads, window, float(sm_scale), float(s_qkv), float(s_a1), float(s_a2), float(s_out), int(r0),
-        int(nr), _stream()), "rel_attention_q8")
+        int(nr), _ptr(v16), _stream()), "rel_attention_q8")
     return out
 

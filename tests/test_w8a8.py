@@ -443,6 +443,46 @@ def test_rel_attention_q8_rows(cuda, window):
 
 
 @pytest.mark.gpu
+def test_w8a8_fp16_v_path(cuda):
+    """Round 6: the qkv GEMM's fp16 copy of the V codes (samq_w8a8_gemm_v16) equals its int8 codes
+    (and leaves them unchanged), the global attention staged from it gives the same codes as from the
+    int8 V, and the W8A8 engine with the path on / off is bit-identical (vit_b, 1024^2)."""
+    from samq import ops
+    from samq.synthetic import random_fq_encoder
+    rng = np.random.Generator(np.random.PCG64(21))
+    heads, d, hw = 12, 64, 64
+    c = heads * d
+    m, k = hw * hw, c
+    a = torch.from_numpy(rng.integers(-128, 128, (m, k), dtype=np.int8)).to(cuda)
+    w = torch.from_numpy(rng.integers(-128, 128, (3 * c, k), dtype=np.int8)).to(cuda)
+    packed = ops.w8_repack(w)
+    ws = torch.from_numpy(rng.random(3 * c, dtype=np.float32) * 1e-3).to(cuda)
+    bias = torch.from_numpy(rng.standard_normal(3 * c, dtype=np.float32) * 0.1).to(cuda)
+    ref = ops.w8a8_gemm(a, packed, ws, 3 * c, bias, ops.EPI_Q8, 0.02, 0.05)
+    for cfg in (0, 89, 90, 84):
+        v16 = torch.full((m, c), 7.0, dtype=torch.float16, device=cuda)
+        got = ops.w8a8_gemm_v16(a, packed, ws, 3 * c, bias, 0.02, 0.05, v16, 2 * c, cfg=cfg)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), cfg
+        assert torch.equal(v16, ref[:, 2 * c:].to(torch.float16)), cfg
+    qkv = ref.view(1, hw, hw, 3 * c)
+    relh = torch.from_numpy((rng.standard_normal((127, d), dtype=np.float32) * 0.5)).to(cuda)
+    relw = torch.from_numpy((rng.standard_normal((127, d), dtype=np.float32) * 0.5)).to(cuda)
+    args = (qkv, None, relh, relw, heads, 0, d ** -0.5, 0.05, 2.0 / 127.5, 6.0 / 127.5, 2.6 / 127.5)
+    o8 = ops.rel_attention_q8(*args)
+    o16 = ops.rel_attention_q8(*args, v16=v16.view(1, hw, hw, c))
+    torch.cuda.synchronize()
+    assert torch.equal(o8, o16)
+    enc = random_fq_encoder("vit_b", device=cuda)
+    eng = enc.engine()
+    img = torch.randn((1, 3, 1024, 1024), generator=torch.Generator(device=cuda).manual_seed(8), device=cuda)
+    eng.v16 = False
+    r0 = eng(img).clone()
+    eng.v16 = True
+    assert torch.equal(eng(img), r0)
+
+
+@pytest.mark.gpu
 def test_w8a8_row_lanes_bit_identical(cuda):
     """Config 2 geometry (vit_b W8A8, 1024^2, B = 1): the engine's opt-in row lanes (grid rows
     [0, 28) and [28, 64) as concurrent kernel chains, joined around the global blocks' attention)

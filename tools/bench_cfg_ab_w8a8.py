@@ -30,6 +30,7 @@ rpw0, lanes0 = eng.ln_rpw, eng.row_lanes   # the engine's defaults are "pick"
 for name, cfg in VARIANTS.items():
     eng.ln_rpw = cfg.get("ln_rpw", rpw0)
     eng.row_lanes = cfg.get("lanes", lanes0)   # round 6: one image as two row lanes
+    eng.v16 = bool(cfg.get("v16", 1))            # round 6: fp16 V copy for the global attention
     for bl in eng.blocks:
         for lay in ("qkv", "proj", "lin1", "lin2"):
             bl[lay]["cfg"] = cfg.get(lay, 0)
