@@ -379,6 +379,18 @@ __device__ __forceinline__ void q8_ptab_fill(uint32_t* ptab, float k2, int lazyc
     ptab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
   }
 }
+// The window kernel's table (round 6): entry 528 + d holds P(d) for d = c - m in [-255, lazyc], entries
+// 0 .. 272 hold 0 -- the masked slots carry the biased code MAG - 400, whose entry -400 - m + 528 is
+// at most 256 for any offset m >= -128 -- so every score, masked or not, is one lookup
+constexpr int PTABW_BASE = 528, PTABW = PTABW_BASE + 256;
+template <int NT>
+__device__ __forceinline__ void q8_ptabw_fill(uint32_t* ptab, float k2, int lazyc, int tid) {
+  for (int i = tid; i <= PTABW_BASE + lazyc; i += NT) {
+    const float pv = i < PTABW_BASE - 255 ? 0.0f : __builtin_amdgcn_exp2f((float)(i - PTABW_BASE) * k2);
+    const _Float16 h = (_Float16)pv, l = (_Float16)(pv - (float)h);
+    ptab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+  }
+}
 // P^T fragments (hi, lo) of 8 scores from their table words (v_perm: two per pair of scores)
 __device__ __forceinline__ void q8_ptab_unpack(const uint32_t (&w)[8], half8_t& bhi, half8_t& blo) {
   uint32_t hi[4], lo[4];
@@ -700,10 +712,10 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
   }
   __syncthreads();   // K / V staged; this wave's rel_h rows visible; q_lds read for the last time
   // the P table (q8_ptab_fill) in q_lds's bytes: the two workgroups per CU leave no room for it
-  static_assert(sizeof(q_lds) >= PTAB * 4, "P table alias");
+  static_assert(sizeof(q_lds) >= PTABW * 4, "P table alias");
   uint32_t* ptab = (uint32_t*)&q_lds[0][0];
   const int lazyc = q8_ptab_lazy(p.k2);
-  q8_ptab_fill<64 * NWQ>(ptab, p.k2, lazyc, tid);
+  q8_ptabw_fill<64 * NWQ>(ptab, p.k2, lazyc, tid);
   __syncthreads();
   const float* rhq = &rh_lds[wave][ql * (SW + 1)];
 
@@ -711,7 +723,11 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
 #pragma unroll
   for (int i = 0; i < 4; ++i) rwr[i] *= inv2;   // see the row64 kernel
   const float lazy = (float)lazyc;
-  int pofs = 0;   // 256 - m (see the row64 kernel)
+  // biased score codes y = MAG + c as in the row64 kernel; masked slots MAG - 400 (table above)
+  constexpr float MAG = 12582912.0f, MASKC = MAG - 400.f;
+  constexpr int MAGB = 0x4B400000;
+  uint32_t tbase = 0;
+  const uint32_t ptab_addr = (uint32_t)(uintptr_t)(SAMQ_LDS void*)ptab;
   const int trow = ql >> 2, tcol = 4 * (ql & 3);
   const half8_t ones = {1, 1, 1, 1, 1, 1, 1, 1};
   float m = -INFINITY;
@@ -729,7 +745,7 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
     for (int bb = 0; bb < 4; ++bb) {
       if (bb >= nb) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) c[bb][i] = -INFINITY;
+        for (int i = 0; i < 4; ++i) c[bb][i] = MASKC;
         continue;
       }
       const int kh = 4 * ch + bb;
@@ -740,8 +756,8 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float q1 = __builtin_amdgcn_fmed3f(__builtin_rintf((float)st[i] * c1), -128.f, 127.f);
-        const float cq = __builtin_amdgcn_fmed3f(__builtin_rintf(fmaf(q1, k12, rh_row + rwr[i])), -128.f, 127.f);
-        c[bb][i] = 4 * g + i < SW ? cq : -INFINITY;
+        const float cq = __builtin_amdgcn_fmed3f(fmaf(q1, k12, rh_row + rwr[i]) + MAG, MAG - 128.f, MAG + 127.f);
+        c[bb][i] = 4 * g + i < SW ? cq : MASKC;
       }
     }
     float cmax = q8max3(c[0][0], c[0][1], c[0][2]);
@@ -759,18 +775,18 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       lacc = lacc * alpha;
       m = cmax;
-      pofs = 256 - (int)cmax;
+      tbase = ptab_addr + 4u * (uint32_t)(PTABW_BASE - (__builtin_bit_cast(int, cmax) - MAGB) - MAGB);
     }
     const _Float16* vb = &v_lds[(ch * 64) * VP];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       if (2 * s2 >= nb) continue;   // both key rows of this k32 step are past the window
       half8_t bhi, blo;
-      uint32_t pw[8];   // masked keys (c = -inf): entry 0, P = 0
+      uint32_t pw[8];   // masked keys (MASKC): an entry below 273, P = 0
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float cv = c[2 * s2 + (j >> 2)][j & 3];
-        pw[j] = ptab[cv == -INFINITY ? 0 : (int)cv + pofs];
+        const uint32_t a = ((uint32_t)__builtin_bit_cast(int, c[2 * s2 + (j >> 2)][j & 3]) << 2) + tbase;
+        pw[j] = *(const SAMQ_LDS uint32_t*)(uintptr_t)a;
       }
       q8_ptab_unpack(pw, bhi, blo);
 #pragma unroll
