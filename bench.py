@@ -58,9 +58,9 @@ def log(*a):
 
 # committed PMC passes (tools/pmc_all.sh) per (mode, GEMM rows per launch), newest round first
 PMC_PROFILES = {("w4a16", 16384): ["r1_pmc_traffic_w4a16.json"],
-                ("w4a16", 8192): ["r5_pmc_traffic_w4a16_m8192.json", "r4_pmc_traffic_w4a16_m8192.json"],
-                ("w4a8", 16384): ["r5_pmc_traffic_w4a8_m16384.json", "r4_pmc_traffic_w4a8_m16384.json"],
-                ("w8a8", 4096): ["r5_pmc_traffic_w8a8_m4096.json", "r4_pmc_traffic_w8a8_m4096.json"]}
+                ("w4a16", 8192): ["r6_pmc_traffic_w4a16_m8192.json", "r5_pmc_traffic_w4a16_m8192.json"],
+                ("w4a8", 16384): ["r6_pmc_traffic_w4a8_m16384.json", "r5_pmc_traffic_w4a8_m16384.json"],
+                ("w8a8", 4096): ["r6_pmc_traffic_w8a8_m4096.json", "r5_pmc_traffic_w8a8_m4096.json"]}
 
 
 def pmc_traffic(mode: str, profiles):
