@@ -371,14 +371,12 @@ constexpr int PTAB = 512;
 __device__ __forceinline__ int q8_ptab_lazy(float k2) {   // lazy offset threshold in codes
   return (int)fminf(floorf(8.0f / k2), 255.0f);
 }
-template <int NT, int PTC = 1>   // PTC interleaved copies: entry i of copy k at word PTC i + k
+template <int NT>
 __device__ __forceinline__ void q8_ptab_fill(uint32_t* ptab, float k2, int lazyc, int tid) {
   for (int i = tid; i <= 256 + lazyc; i += NT) {
     const float pv = i == 0 ? 0.0f : __builtin_amdgcn_exp2f((float)(i - 256) * k2);
     const _Float16 h = (_Float16)pv, l = (_Float16)(pv - (float)h);
-    const uint32_t w = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
-#pragma unroll
-    for (int k = 0; k < PTC; ++k) ptab[PTC * i + k] = w;
+    ptab[i] = (uint32_t)__builtin_bit_cast(uint16_t, h) | ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
   }
 }
 // The window kernel's table (round 6): entry 528 + d holds P(d) for d = c - m in [-255, lazyc], entries
@@ -417,21 +415,11 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   constexpr int UNITS = KC * 4;                  // 16-byte pieces of one chunk's K (and of its V)
   static_assert(UNITS % NT == 0, "staging");
   constexpr int UPT = UNITS / NT;
-  // P table in PTC interleaved copies (entry e of copy k at word PTC e + k, lane l reads copy l % PTC):
-  // the 16 table reads per wave and key row are random gathers, and with one copy their bank
-  // conflicts were half of the kernel's LDS cycles (SQ_LDS_BANK_CONFLICT, profiles/r6_w8a8_attention_v16.log);
-  // the Q-code staging (prologue only) lives in V buffer 1, so three workgroups still fit a CU
-#ifdef SAMQ_TUNING
-  constexpr int PTC = 1;   // A/B: the round-5 single table
-#else
-  constexpr int PTC = 4;
-#endif
   __shared__ __attribute__((aligned(16))) int8_t k_lds[2][KC * KPITCH];
   __shared__ __attribute__((aligned(16))) _Float16 v_lds[2][KC * VP];
+  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
   __shared__ float rh_lds[NWQ][16 * (G + 1)];
-  __shared__ uint32_t ptab[PTAB * PTC];
-  static_assert(NWQ * 16 * KPITCH <= KC * VP * 2, "Q staging alias");
-  int8_t (*q_lds)[16 * KPITCH] = (int8_t (*)[16 * KPITCH])&v_lds[1][0];
+  __shared__ uint32_t ptab[PTAB];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -443,7 +431,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   const int b = blockIdx.x;
   const int qy = p.row0 + blockIdx.z;           // query grid row of this workgroup
   const int lazyc = q8_ptab_lazy(p.k2);
-  q8_ptab_fill<NT, PTC>(ptab, p.k2, lazyc, tid);   // visible after the first barrier below
+  q8_ptab_fill<NT>(ptab, p.k2, lazyc, tid);     // visible after the first barrier below
   const int qx = wave * 16 + ql;
   const int64_t ts = 3 * (int64_t)C;
   const int8_t* img = p.qkv + (int64_t)b * G * G * ts;
@@ -535,7 +523,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   // LDS byte address of the P-table entry of code y: (bits(y) << 2) + tbase, tbase = ptab + 4 (256 -
   // m_code - MAGB) (mod 2^32)
   uint32_t tbase = 0;
-  const uint32_t ptab_addr = (uint32_t)(uintptr_t)(SAMQ_LDS void*)ptab + 4u * (uint32_t)(lane % PTC);
+  const uint32_t ptab_addr = (uint32_t)(uintptr_t)(SAMQ_LDS void*)ptab;
   float4_t acc[QD / 16], lacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int t = 0; t < QD / 16; ++t) acc[t] = float4_t{0.f, 0.f, 0.f, 0.f};
@@ -574,13 +562,13 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
       for (int t = 0; t < QD / 16; ++t) acc[t] = acc[t] * alpha;
       lacc = lacc * alpha;
       m = cmax;
-      tbase = ptab_addr + 4u * PTC * (uint32_t)(256 - (__builtin_bit_cast(int, cmax) - MAGB) - MAGB);
+      tbase = ptab_addr + 4u * (uint32_t)(256 - (__builtin_bit_cast(int, cmax) - MAGB) - MAGB);
     }
     // ---- P (hi + lo fp16, from the table) and O^T += V^T.P^T, l += ones.P^T, two 32-key steps
     uint32_t pw[2][8];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const uint32_t a = ((uint32_t)__builtin_bit_cast(int, c[j >> 2][j & 3]) * (4u * PTC)) + tbase;
+      const uint32_t a = ((uint32_t)__builtin_bit_cast(int, c[j >> 2][j & 3]) << 2) + tbase;
       pw[j >> 3][j & 7] = *(const SAMQ_LDS uint32_t*)(uintptr_t)a;
     }
     const _Float16* vb = &v_lds[buf][0];
