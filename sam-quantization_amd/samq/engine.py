@@ -104,6 +104,9 @@ class EncoderEngine:
             for p in self.plans:
                 for lin in (p.qkv, p.proj, p.lin1, p.lin2):
                     lin.prepare_w4a8()
+            # LN-q at four rows per wave in the 2-lane W4A8 graph: 34.58 vs 34.80 ms and 34.83 vs 34.99
+            # (two boxes, interleaved, bit-identical, profiles/r6_ln_rpw_w4a8_ab.log); W4A16 keeps 2
+            self.ln_rpw = 4
         self._fold_ready = False
         pe = enc.patch_embed.proj
         self.patch = pe.kernel_size[0]
