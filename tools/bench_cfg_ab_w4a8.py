@@ -32,9 +32,10 @@ eng = enc.engine()
 g = torch.Generator(device=dev).manual_seed(1234)
 img = torch.randn((8, 3, 1024, 1024), generator=g, device=dev, dtype=torch.float16)
 graphs, ref = {}, None
+rpw0 = eng.ln_rpw   # the engine's default is "pick"
 for name, cfg in VARIANTS.items():
     eng.res_mode = cfg.get("res", "epi")
-    eng.ln_rpw = cfg.get("ln_rpw", 0)
+    eng.ln_rpw = cfg.get("ln_rpw", rpw0)
     eng.lane_priority = cfg.get("prio", 0)   # round 6: lane 0's stream at high priority
     eng.rowsums = {0: False, 1: True, 2: "ln"}[cfg.get("rowsums", 1)]   # round 6: producer-side row sums
     eng.skip = frozenset(k[5:] for k in cfg if k.startswith("skip_"))   # timing-only
