@@ -48,7 +48,7 @@ __device__ __forceinline__ float aq8(float v, float s) {
 constexpr int QD = 64;       // head dim (vit_b)
 
 __device__ __forceinline__ float q8max3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
-constexpr int KPITCH = 80;   // K row pitch in LDS (bytes): conflict-free 16-byte fragment reads
+constexpr int KPITCH = 80;   // K row pitch in LDS (bytes) of the generic kernel (the row64 / window kernels use 96)
 
 // ROW64: global attention over a 64-wide grid -- a 64-key chunk is exactly one key row, so the
 // height term is one value per chunk and the width term a fixed per-lane set (registers).
@@ -408,16 +408,26 @@ __device__ __forceinline__ void q8_ptab_unpack(const uint32_t (&w)[8], half8_t& 
 // (round 6): the second quantiser rounds by adding 1.5 * 2^23 (exact round-half-even for |x| < 2^22)
 // and clamps in that biased form, so a code's P-table address is one v_lshl_add of its bits -- no
 // float -> int conversion per score.
+// LDS pitches (round 6, second pass): K rows at 96 bytes -- the ds_read_b128 fragment reads are then
+// conflict-free in all four lane groups (at 80 bytes three lane pairs of every group shared a bank) --
+// and V rows at 80 halves, which takes the tr reads of key quads 0 / 7 off the same banks (72 made
+// every tr read 2-way); the query staging of the prologue aliases V buffer 1 (unused until the first
+// key row's store, after the prologue barrier), so three workgroups still fit a CU.  Kernel 120.3 ->
+// 118.5 us per vit_b launch, bit-identical (profiles/r6_w8a8_row64_variants.log; that log also holds
+// the measured-slower speculative P-table reads and the LDS-free direct-from-L2 prototype).
 template <int NWQ, bool V16 = false>
 __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(AttnQ8Params p) {
-  constexpr int G = 64, KC = 64, VP = QD + 8;    // V row pitch (halves): spreads the tr reads over banks
+  constexpr int G = 64, KC = 64;
+  constexpr int KP = 96;                         // K row pitch (bytes)
+  constexpr int VP = QD + 16;                    // V row pitch (halves)
   constexpr int NT = 64 * NWQ;
   constexpr int UNITS = KC * 4;                  // 16-byte pieces of one chunk's K (and of its V)
   static_assert(UNITS % NT == 0, "staging");
   constexpr int UPT = UNITS / NT;
-  __shared__ __attribute__((aligned(16))) int8_t k_lds[2][KC * KPITCH];
+  __shared__ __attribute__((aligned(16))) int8_t k_lds[2][KC * KP];
   __shared__ __attribute__((aligned(16))) _Float16 v_lds[2][KC * VP];
-  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
+  int8_t(*q_lds)[16 * KP] = (int8_t(*)[16 * KP])(void*)&v_lds[1][0];   // prologue only
+  static_assert(NWQ * 16 * KP <= KC * VP * 2, "query staging inside V buffer 1");
   __shared__ float rh_lds[NWQ][16 * (G + 1)];
   __shared__ uint32_t ptab[PTAB];
 
@@ -460,7 +470,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
 #pragma unroll
     for (int j = 0; j < UPT; ++j) {
       const int u = tid + j * NT, key = u >> 2, part = u & 3;
-      *(u32x4*)(&k_lds[buf][key * KPITCH + part * 16]) = kreg[r][j];
+      *(u32x4*)(&k_lds[buf][key * KP + part * 16]) = kreg[r][j];
       if constexpr (V16) {
         *(u32x4*)(&v_lds[buf][key * VP + part * 16]) = vreg[r][2 * j];
         *(u32x4*)(&v_lds[buf][key * VP + part * 16 + 8]) = vreg[r][2 * j + 1];
@@ -485,13 +495,13 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
   // reads, rel_h into LDS (one value per key row per chunk); no rel_w table in LDS, so three
   // workgroups fit a CU (the 768 workgroups of a vit_b launch are then all resident at once).
   const int4v qfrag = *(const int4v*)(img + ((int64_t)qy * G + qx) * ts + head * QD + g * 16);
-  *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
+  *(int4v*)(&q_lds[wave][ql * KP + g * 16]) = qfrag;
   __builtin_amdgcn_s_waitcnt(0xC07F);
   float rwr[4][4];
 #pragma unroll
   for (int bb = 0; bb < 4; ++bb) {
     float4_t rh4, rw4;
-    q8_rel_block(p, &q_lds[wave][ql * KPITCH], qy, G, bb, lane, rh4, rw4);
+    q8_rel_block(p, &q_lds[wave][ql * KP], qy, G, bb, lane, rh4, rw4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       rh_lds[wave][ql * (G + 1) + 16 * bb + 4 * g + i] = rh4[i];
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
     float c[4][4];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
-      const int4v kf = *(const int4v*)(&k_lds[buf][(bb * 16 + ql) * KPITCH + g * 16]);
+      const int4v kf = *(const int4v*)(&k_lds[buf][(bb * 16 + ql) * KP + g * 16]);
       const int4v z = {0, 0, 0, 0};
       const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
 #pragma unroll
@@ -622,13 +632,13 @@ __global__ __launch_bounds__(64 * NWQ, 3) void rel_attention_q8_row64_kernel(Att
 template <int SW, int NWQ = SW>
 // two workgroups per CU: LDS <= 80 KiB and (HIP's second bound = waves per SIMD) <= 512 / (waves / 2) VGPRs
 __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_win_kernel(AttnQ8Params p) {
-  constexpr int SLOTS = 16 * SW, VP = QD + 8;
+  constexpr int SLOTS = 16 * SW, KP = 96, VP = QD + 16;   // conflict-free pitches: see the row64 kernel
   static_assert(SW % NWQ == 0, "query rows split evenly");
   constexpr int NCH = (SW + 3) / 4;                        // chunks of up to 4 key rows (64 slots)
   static_assert(SW <= 16, "one window per workgroup");
-  __shared__ __attribute__((aligned(16))) int8_t k_lds[SLOTS * KPITCH];
+  __shared__ __attribute__((aligned(16))) int8_t k_lds[SLOTS * KP];
   __shared__ __attribute__((aligned(16))) _Float16 v_lds[SLOTS * VP];
-  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KPITCH];
+  __shared__ __attribute__((aligned(16))) int8_t q_lds[NWQ][16 * KP];
   __shared__ float rh_lds[NWQ][16 * (SW + 1)];
 
   const int tid = threadIdx.x;
@@ -669,7 +679,7 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
         }
       }
     }
-    *(u32x4*)(&k_lds[slot * KPITCH + part * 16]) = kc;
+    *(u32x4*)(&k_lds[slot * KP + part * 16]) = kc;
     half8_t h0, h1;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -698,12 +708,12 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
       }
     }
   }
-  *(int4v*)(&q_lds[wave][ql * KPITCH + g * 16]) = qfrag;
+  *(int4v*)(&q_lds[wave][ql * KP + g * 16]) = qfrag;
   __builtin_amdgcn_s_waitcnt(0xC07F);
   float rwr[4];
   {
     float4_t rh4, rw4;
-    q8_rel_block(p, &q_lds[wave][ql * KPITCH], qy, SW, 0, lane, rh4, rw4);
+    q8_rel_block(p, &q_lds[wave][ql * KP], qy, SW, 0, lane, rh4, rw4);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       rwr[i] = rw4[i];
@@ -750,7 +760,7 @@ __global__ __launch_bounds__(64 * NWQ, (2 * NWQ + 3) / 4) void rel_attention_q8_
       }
       const int kh = 4 * ch + bb;
       const float rh_row = rhq[kh] * inv2;
-      const int4v kf = *(const int4v*)(&k_lds[(kh * 16 + ql) * KPITCH + g * 16]);
+      const int4v kf = *(const int4v*)(&k_lds[(kh * 16 + ql) * KP + g * 16]);
       const int4v z = {0, 0, 0, 0};
       const int4v st = __builtin_amdgcn_mfma_i32_16x16x64_i8(kf, qfrag, z, 0, 0, 0);
 #pragma unroll
